@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""Headline benchmark: two-pass Lanczos f(A)b on the 500k-arc rho=3 netgen KKT instance,
+k = 500, f = inv (BASELINE.json configs[2]; metric "Lanczos iterations/sec + SpMV GB/s
+(vs HBM roofline), 500k-arc KKT k=500").
+
+A "step" = one full ``solvers::lanczos_two_pass`` call (pass one, host f(T_k) solve,
+pass two), the window the reference times (src/bin/tradeoff.rs:265-288). Inputs
+(A, b) are resident in HBM before the timed region; x stays in HBM.
+
+    python bench.py [--gpus N --steps K --warmup W]
+
+N > 1 (launched by torch.distributed.run, one rank per GPU): every rank runs its own
+full-size replica of the workload (no data-path collective),
+timed between barriers, max over ranks; value = all ranks' iterations / that time.
+
+Extra JSON fields: ``roofline`` for the dominant kernel (algorithmic bytes per launch /
+HIP-event average launch time, vs 8 TB/s HBM3E), ``cpu_baseline`` (the oracle's
+reference-order restatement, single core, bounded sample on the host of the GPU box).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "two-pass-lanczos_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+METRIC = "Lanczos iterations/sec + SpMV GB/s (vs HBM roofline), 500k-arc KKT k=500"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--k", type=int, default=500)
+    p.add_argument("--arcs", type=int, default=500000, choices=[5000, 50000, 500000])
+    p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU leg")
+    p.add_argument("--cpu-k", type=int, default=500, help="k of the bounded CPU sample")
+    p.add_argument("--cpu-reps", type=int, default=2, help="CPU sample repetitions")
+    p.add_argument("--profile-iters", type=int, default=200)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")  # barriers / max-reduce of host timings only
+
+    import numpy as np
+    import torch
+
+    import tpl_amd
+    from tpl_amd import _lib
+    from tpl_amd.error import check
+    from tpl_amd.utils.data_loader import load_kkt_system, write_qfc_3line
+
+    torch.cuda.set_device(local_rank)
+    dmx = os.path.join(ROOT, "tests", "golden", "kkt", f"netgen-{args.arcs}-3.dmx.xz")
+    qfc = os.path.join("/tmp", f"tpl_bench_{args.arcs}_{os.getpid()}.qfc")
+    write_qfc_3line(qfc, args.arcs)
+    kkt = load_kkt_system(dmx, qfc)
+    os.unlink(qfc)
+    a = kkt.a
+    n = a.shape[0]
+    b = a @ np.full(n, 1.0 / np.sqrt(n))  # src/bin/tradeoff.rs:235-236
+
+    op = tpl_amd.HipCsrOp(a, device=local_rank)
+    b_dev = torch.from_numpy(b).cuda(local_rank)
+    x_dev = torch.empty_like(b_dev)
+    torch.cuda.synchronize()
+
+    def solve():
+        check(_lib.tpl_lanczos_two_pass(op.handle, b_dev.data_ptr(), n, args.k, _lib.FTK_INV_PTR,
+                                        None, x_dev.data_ptr(), _lib.TPL_MEM_DEVICE))
+
+    for _ in range(max(args.warmup, 0)):
+        solve()
+    dec = tpl_amd.algorithms.lanczos_pass_one(op, b, args.k)
+    steps_taken = dec.steps_taken
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        solve()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+
+    # ---- roofline of the dominant kernel (HIP events on the operator's stream)
+    launches = {_lib.TPL_KERNEL_PASS1_SPMV: steps_taken, _lib.TPL_KERNEL_PASS1_AXPY: steps_taken,
+                _lib.TPL_KERNEL_PASS2_SPMV: steps_taken - 1}
+    names = {_lib.TPL_KERNEL_PASS1_SPMV: "k_p1_spmv", _lib.TPL_KERNEL_PASS1_AXPY: "k_p1_axpy",
+             _lib.TPL_KERNEL_PASS2_SPMV: "k_p2_spmv"}
+    prof = {}
+    for kid in launches:
+        us, by = op.profile_kernel(kid, args.profile_iters)
+        prof[kid] = (us, by)
+    dom = max(launches, key=lambda kk: prof[kk][0] * launches[kk])
+    us, by = prof[dom]
+    achieved = by / (us * 1e-6) / 1e9
+
+    iters = args.steps * steps_taken * world
+    value = iters / dt
+    out = {
+        "metric": METRIC,
+        "value": round(value, 2),
+        "unit": "Lanczos iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1000.0 * dt / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "netgen 500k-arc rho=3 instance regenerated from the reference's netgen "
+                "(tests/golden/kkt), b = A(1/sqrt(n))1, qfc 3-line (D empty)",
+        "config": {"workload": f"lanczos_two_pass k={args.k} f=inv, {args.arcs}-arc rho=3 KKT "
+                               f"(n={n}, nnz={a.nnz})",
+                   "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
+                   "parallelism": "single" if world == 1 else f"replicas{world}"},
+        "roofline": {"bound": "hbm", "kernel": names[dom], "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "algo_bytes_per_launch": by,
+                     "avg_launch_us_events": round(us, 3),
+                     "kernels_us": {names[kk]: round(prof[kk][0], 3) for kk in prof}},
+    }
+
+    if rank == 0 and args.cpu_baseline:
+        import oracle  # CPU baseline only (reference-order restatement, single thread)
+        from oracle import ftk_ref
+        o = oracle.Operator(a)
+        kc = min(args.cpu_k, args.k)
+        reps = max(1, args.cpu_reps)
+        t1 = time.perf_counter()
+        for _ in range(reps):
+            o.lanczos_two_pass(b, kc, ftk_ref.inv)
+        tc = (time.perf_counter() - t1) / reps
+        out["cpu_baseline"] = {
+            "value": round(kc / tc, 2), "unit": "Lanczos iterations/s", "cores": 1,
+            "kind": "port",
+            "sample": f"oracle C restatement (reference order, gcc -O2, 1 thread) "
+                      f"lanczos_two_pass k={kc} f=inv on the same instance, {reps} calls, "
+                      f"{tc:.2f} s/call",
+        }
+        out["speedup_vs_cpu"] = round(value / (kc / tc), 1)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,214 @@
+/*
+ * tpl.h — C ABI of the MI355X two-pass Lanczos engine (libtpl_amd.so).
+ *
+ * This is the drop-in boundary for the hot path of lukefleed/two-pass-lanczos:
+ * the Lanczos recurrence behind `solvers::lanczos` / `solvers::lanczos_two_pass`
+ * and the low-level `algorithms::*` entry points. Every entry point below names
+ * the reference item it replaces (file:line under the reference checkout).
+ * The signatures are plain C (pointers + sizes, no torch / HIP types), so a
+ * Rust `extern "C"` block, ctypes, or a C++ caller can bind them directly
+ * (bindings: INTEGRATION.md).
+ *
+ * Conventions
+ *   - All arithmetic is IEEE fp64 (every reference call site is f64).
+ *   - Vectors `b`, `x_out`, `v_out` are host pointers when `mem == TPL_MEM_HOST`
+ *     and device pointers on the operator's GPU when `mem == TPL_MEM_DEVICE`.
+ *     Scalar arrays (alphas, betas, y) are always host pointers.
+ *   - `v_out` matrices are column-major n x steps (leading dimension n), the
+ *     layout of the reference's `Mat<f64>` V_k.
+ *   - Every function returns a tpl_status; on failure tpl_last_error() returns
+ *     the message, formatted exactly like the reference's `Display` strings
+ *     (src/error.rs:20-58) for the Lanczos error kinds.
+ *   - An operator owns one HIP stream and its device workspace; calls on one
+ *     operator are not re-entrant (the reference is single-threaded, Par::Seq).
+ */
+#ifndef TPL_H_
+#define TPL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- status codes: mirror LanczosErrorKind (src/error.rs:20-58) ---------- */
+typedef enum tpl_status {
+  TPL_OK = 0,
+  TPL_ERR_BREAKDOWN = 1,           /* LanczosErrorKind::Breakdown (declared, never constructed by the reference) */
+  TPL_ERR_DIMENSION_MISMATCH = 2,  /* LanczosErrorKind::DimensionMismatch (reference panics instead; we report) */
+  TPL_ERR_INPUT = 3,               /* LanczosErrorKind::InputError  (src/algorithms/mod.rs:268-272, lanczos_two_pass.rs:229-235) */
+  TPL_ERR_PARAMETER_MISMATCH = 4,  /* LanczosErrorKind::ParameterMismatch (src/solvers.rs:78-85,158-165; lanczos_two_pass.rs:220-227) */
+  TPL_ERR_EVD = 5,                 /* LanczosErrorKind::EvdError (built-in exp solver only) */
+  TPL_ERR_SOLVER = 6,              /* LanczosErrorKind::SolverError (src/solvers.rs:75,156) */
+  /* engine / loader errors (no reference counterpart in LanczosErrorKind) */
+  TPL_ERR_INVALID_ARGUMENT = 100,
+  TPL_ERR_DEVICE = 101,            /* HIP runtime failure; message carries hipGetErrorString */
+  TPL_ERR_OUT_OF_MEMORY = 102,
+  TPL_ERR_DATA_LOADER = 103,       /* DataLoaderError (src/utils/data_loader.rs:16-43) */
+  TPL_ERR_UNSUPPORTED = 104
+} tpl_status;
+
+enum { TPL_MEM_HOST = 0, TPL_MEM_DEVICE = 1 };
+
+typedef struct tpl_ctx_s* tpl_ctx_t; /* one GPU + one HIP stream          */
+typedef struct tpl_op_s* tpl_op_t;   /* device-resident CSR operator A    */
+
+/* Thread-local message of the last failing call ("" after success). */
+const char* tpl_last_error(void);
+/* Library version string, e.g. "tpl_amd 0.1.0 gfx950". */
+const char* tpl_version(void);
+
+/* ---- context ------------------------------------------------------------- */
+tpl_status tpl_ctx_create(int device, tpl_ctx_t* out);
+tpl_status tpl_ctx_destroy(tpl_ctx_t ctx);
+/* Synchronise the context stream (all operators created on it share it). */
+tpl_status tpl_ctx_synchronize(tpl_ctx_t ctx);
+/* Number of visible GPUs (0 on a host without one; never fails). */
+int tpl_device_count(void);
+
+/* ---- operator: replaces faer `LinOp<f64>` for `SparseColMatRef<usize,f64>`
+ *      (used at src/algorithms/mod.rs:177, src/algorithms/lanczos_two_pass.rs:186).
+ *  A must be square n x n and SYMMETRIC (the Lanczos contract; A = [[D,E^T],[E,0]]
+ *  for the KKT inputs), so its CSR arrays equal the reference's CSC arrays.
+ *  Host arrays are borrowed for the call only; the operator copies them to HBM.
+ *  Column indices must be sorted ascending within each row, 0 <= col < n.
+ *  Limits: nnz < 2^31 (int32 offsets on device).                               */
+tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz,
+                             const int64_t* row_ptr, const int32_t* col_idx,
+                             const double* vals, tpl_op_t* out);
+tpl_status tpl_op_destroy(tpl_op_t op);
+int64_t tpl_op_nrows(tpl_op_t op); /* LinOp::nrows / ncols */
+int64_t tpl_op_nnz(tpl_op_t op);
+
+/* y = A x  — LinOp::apply (compatibility path; the solvers below keep the whole
+ * recurrence on the device and never call this per step).                     */
+tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem);
+
+/* ---- f(T_k) solver callback: replaces the `f_tk_solver` closure
+ *      `FnMut(&[f64], &[f64]) -> Result<Mat<f64>, anyhow::Error>` (src/solvers.rs:57,144).
+ *  Called exactly once per solve, after pass one, with n_alphas = steps and
+ *  n_betas = steps - 1. Write y' = f(T_k) e_1 into y_out (capacity y_cap = steps)
+ *  and its length into *y_len. Return 0 on success; non-zero means Err(e): put
+ *  e's text (NUL-terminated) into err_msg (capacity err_cap).                   */
+typedef int (*tpl_ftk_fn)(const double* alphas, size_t n_alphas, const double* betas,
+                          size_t n_betas, double* y_out, size_t y_cap, size_t* y_len,
+                          char* err_msg, size_t err_cap, void* user);
+
+/* Built-in f(T_k) solvers with the tpl_ftk_fn signature (user ignored):
+ *  inv : y' = T_k^{-1} e_1, tridiagonal LU with partial pivoting
+ *        (the harness's sp_lu / partial_piv_lu, src/bin/tradeoff.rs:245-258,
+ *        tests/correctness.rs:171-179). A singular T_k yields non-finite y'
+ *        exactly like an LU solve does (no error), matching the reference.
+ *  exp : y' = Q exp(Lambda) Q^T e_1 via symmetric tridiagonal QL eigensolver
+ *        (src/bin/stability.rs:175-193). Non-convergence -> non-zero return.
+ *  sq  : y' = T_k^2 e_1 (tests/correctness.rs:287-299).                        */
+int tpl_ftk_inv(const double* alphas, size_t n_alphas, const double* betas, size_t n_betas,
+                double* y_out, size_t y_cap, size_t* y_len, char* err_msg, size_t err_cap,
+                void* user);
+int tpl_ftk_exp(const double* alphas, size_t n_alphas, const double* betas, size_t n_betas,
+                double* y_out, size_t y_cap, size_t* y_len, char* err_msg, size_t err_cap,
+                void* user);
+int tpl_ftk_sq(const double* alphas, size_t n_alphas, const double* betas, size_t n_betas,
+               double* y_out, size_t y_cap, size_t* y_len, char* err_msg, size_t err_cap,
+               void* user);
+
+/* ---- high-level API: src/solvers.rs ------------------------------------- */
+/* solvers::lanczos (src/solvers.rs:46-107): standard pass (V_k kept in HBM),
+ * f(T_k) on the host, x = ||b|| V_k y' (device GEMV). x_out has n entries.     */
+tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                       tpl_ftk_fn f, void* f_user, double* x_out, int mem);
+/* solvers::lanczos_two_pass (src/solvers.rs:133-175): pass one (scalars only),
+ * f(T_k) on the host, y = y' ||b||, pass two regenerates V_k on the fly.        */
+tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                                tpl_ftk_fn f, void* f_user, double* x_out, int mem);
+
+/* ---- low-level API: src/algorithms/ -------------------------------------- */
+/* Per-step callback of lanczos_standard (LanczosCallback, src/algorithms/mod.rs:82-86):
+ * called after every step with k = steps so far (1-based), the DEVICE pointer of
+ * V_k (column-major, ld = n, k valid columns) and the host T_k scalars
+ * (k alphas, k-1 betas... exactly the reference's TridiagonalSystemView, i.e.
+ * betas holds the betas pushed so far). Return non-zero to continue, 0 to stop.
+ * Supplying a callback forces one host synchronisation per step (slow path).   */
+typedef int (*tpl_step_cb)(size_t k, const double* v_k_device, int64_t n,
+                           const double* alphas, size_t n_alphas, const double* betas,
+                           size_t n_betas, void* user);
+
+/* algorithms::lanczos::lanczos_standard (src/algorithms/lanczos.rs:55-156).
+ * alphas: capacity k; betas: capacity k (k-1 used); v_out: n x k capacity or NULL.
+ * On return *steps = steps_taken, *b_norm = ||b||, alphas[0..steps), betas[0..steps-1),
+ * v_out columns [0, steps) filled. reorth != 0 enables full re-orthogonalisation
+ * (CGS2 against the stored V_k; an extension with no reference counterpart).   */
+tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                                double* alphas, double* betas, size_t* steps,
+                                double* b_norm, double* v_out, int mem, int reorth,
+                                tpl_step_cb cb, void* cb_user);
+
+/* algorithms::lanczos_two_pass::lanczos_pass_one (src/algorithms/lanczos_two_pass.rs:65-110). */
+tpl_status tpl_lanczos_pass_one(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                                double* alphas, double* betas, size_t* steps,
+                                double* b_norm, int mem);
+
+/* algorithms::lanczos_two_pass::lanczos_pass_two (:128-140) and, with v_out != NULL,
+ * lanczos_pass_two_with_basis (:149-166). The decomposition is passed as its
+ * fields (LanczosDecomposition, src/algorithms/mod.rs:94-108); y = y_k (already
+ * scaled by ||b||) with y_len entries. x_out: n entries; v_out: n x steps or NULL. */
+tpl_status tpl_lanczos_pass_two(tpl_op_t op, const double* b, int64_t b_len,
+                                const double* alphas, size_t n_alphas, const double* betas,
+                                size_t n_betas, size_t steps, double b_norm,
+                                const double* y, size_t y_len, double* x_out,
+                                double* v_out, int mem);
+
+/* ---- data loader: src/utils/data_loader.rs:211-259 (load_kkt_system) ----- */
+typedef struct tpl_csr_host {
+  int64_t n, nnz;
+  int64_t num_nodes, num_arcs; /* KKTSystem::num_nodes / num_arcs */
+  int64_t* row_ptr;            /* n + 1 */
+  int32_t* col_idx;            /* nnz, ascending within each row  */
+  double* vals;                /* nnz */
+} tpl_csr_host;
+/* Parse a DIMACS .dmx + .qfc pair with the reference's exact semantics
+ * (node-index 0 rejected; .qfc read as line 1 = m, then `skip(m).take(m)`
+ * one-float-per-line — so the 3-line qfcgen format yields D = empty) and
+ * assemble A = [[D, E^T],[E, 0]] as CSR. Free with tpl_csr_host_free.          */
+tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_csr_host* out);
+void tpl_csr_host_free(tpl_csr_host* csr);
+
+/* ---- introspection / measurement ---------------------------------------- */
+/* Schedule of the fused SpMV kernels: G persistent workgroups walk n_items row
+ * items (kind 0 = stream rows, 1 = one wave per row, 2 = one block per row);
+ * E = elements per workgroup of the element-wise kernels. items_out may be NULL
+ * (then only the counts are returned); else 4 int32 per item:
+ * {row0, row1, nz0, kind}. The CPU oracle uses this to reproduce the device
+ * reduction order bit for bit.                                                 */
+tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_items, int32_t* G, int32_t* E,
+                           int32_t* items_out);
+/* Schedule tuning (before the first solve; rebuilds the item list):
+ * stream_nnz_cap <= 2048, stream_rows_cap <= 1024, max_groups >= 1 (0 = default). */
+tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t stream_nnz_cap, int32_t stream_rows_cap,
+                               int32_t wave_row_max, int32_t max_groups);
+
+/* Kernel ids for tpl_profile_kernel */
+enum {
+  TPL_KERNEL_PASS1_SPMV = 0, /* fused SpMV + beta-AXPY + alpha partials (pass one) */
+  TPL_KERNEL_PASS1_AXPY = 1, /* alpha-AXPY + ||w||^2 partials (pass one)          */
+  TPL_KERNEL_PASS2_SPMV = 2, /* fused SpMV + both AXPYs + scale + x += y v (pass two) */
+  TPL_KERNEL_SPMV = 3        /* plain y = A x                                      */
+};
+/* Time `iters` back-to-back launches of one kernel on the operator's stream with
+ * HIP events (a warm-up launch first). Returns the average per launch in
+ * microseconds (event-to-event, so it includes the launch gap) and the
+ * algorithmic bytes one launch moves ("Algorithmic bytes").          */
+tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us,
+                              double* algo_bytes);
+/* Algorithmic bytes of one launch of `kernel` (no GPU work). */
+double tpl_kernel_algo_bytes(tpl_op_t op, int kernel);
+
+/* Blocking copy of `bytes` from device memory to host memory (used by callbacks
+ * that receive device views, e.g. tpl_step_cb's V_k). */
+tpl_status tpl_copy_to_host(void* dst, const void* src_device, size_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TPL_H_ */

@@ -1,0 +1,280 @@
+/*
+ * lanczos_oracle.c — CPU ORACLE (test infrastructure only; never shipped, never
+ * on the product path). Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load it.
+ *
+ * A plain-C restatement of the reference's Lanczos hot path
+ * (lukefleed/two-pass-lanczos, Rust + faer 0.22.6, unbuildable here: no cargo):
+ *   recurrence step   src/algorithms/mod.rs:167-212   (apply, -beta v_prev, alpha, -alpha v, ||w||)
+ *   iteration state   src/algorithms/mod.rs:261-340   (v1 = b * (1/||b||), v = w * (1/beta))
+ *   breakdown tol     src/algorithms/mod.rs:140-143   (1000 * f64::EPSILON, absolute)
+ *   standard          src/algorithms/lanczos.rs:55-156
+ *   pass one          src/algorithms/lanczos_two_pass.rs:65-110
+ *   pass two          src/algorithms/lanczos_two_pass.rs:176-312
+ *   reconstruction    src/solvers.rs:96-104           (x = ||b|| V_k y')
+ *
+ * Two reduction modes (everything else — the elementwise AXPY/scale rounding —
+ * is identical in both and follows the reference op by op):
+ *   FAITHFUL  (sched == NULL): CSR row-sequential ascending-column SpMV (the
+ *             natural faer CSC scatter order), sequential dot and sum of
+ *             squares. faer's own SIMD summation order is not pinned (its source
+ *             is not vendored), so this is the "reference order" up to faer's
+ *             dot/norm association — the CPU baseline of bench.py.
+ *   CANONICAL (sched != NULL): reproduces the device's fixed reduction trees
+ *             (two-pass-lanczos_amd/csrc/tpl_device.h) bit for bit, given the
+ *             operator's item schedule (tpl_op_schedule).
+ *
+ * Build: make -C oracle (gcc, -ffp-contract=off so a*b-c stays two roundings).
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define TPB 256
+#define TOL 2.220446049250313080847263336181640625e-13 /* 1000 * f64::EPSILON */
+
+enum { OR_OK = 0, OR_ZERO_B = 3, OR_BAD = 100 };
+
+typedef struct {
+  int64_t n;
+  const int64_t* rp;
+  const int32_t* ci;
+  const double* v;
+} ocsr;
+
+typedef struct {
+  int32_t n_items;
+  const int32_t* items; /* 4 per item: row0, row1, nz0, kind (0 stream, 1 wave, 2 block) */
+  int32_t G;
+  int64_t E;
+} osched;
+
+/* ------------------------------------------------------------ trees */
+static double tree64(double* a) { /* xor butterfly == pairwise (l, l+half) tree */
+  for (int half = 32; half >= 1; half >>= 1)
+    for (int l = 0; l < half; ++l) a[l] = a[l] + a[l + half];
+  return a[0];
+}
+static double tree256(const double* a) {
+  double w[4], tmp[64];
+  for (int q = 0; q < 4; ++q) {
+    memcpy(tmp, a + 64 * q, sizeof(tmp));
+    w[q] = tree64(tmp);
+  }
+  return (w[0] + w[1]) + (w[2] + w[3]);
+}
+static double reduce_partials(const double* P, int G) {
+  double s[TPB];
+  for (int t = 0; t < TPB; ++t) {
+    s[t] = 0.0;
+    for (int i = t; i < G; i += TPB) s[t] = s[t] + P[i];
+  }
+  return tree256(s);
+}
+
+/* ------------------------------------------------------------ SpMV */
+static void spmv_faithful(const ocsr* A, const double* x, double* y) {
+  for (int64_t i = 0; i < A->n; ++i) {
+    double s = 0.0;
+    for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
+    y[i] = s;
+  }
+}
+
+static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* y) {
+  double acc[TPB];
+  for (int32_t it = 0; it < S->n_items; ++it) {
+    const int32_t* I = S->items + 4 * it;
+    const int32_t row0 = I[0], row1 = I[1], kind = I[3];
+    if (kind == 0) {
+      for (int32_t i = row0; i < row1; ++i) {
+        double s = 0.0;
+        for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
+        y[i] = s;
+      }
+    } else if (kind == 1) {
+      for (int32_t i = row0; i < row1; ++i) {
+        double lane[64];
+        for (int l = 0; l < 64; ++l) {
+          double s = 0.0;
+          for (int64_t q = A->rp[i] + l; q < A->rp[i + 1]; q += 64) s = s + A->v[q] * x[A->ci[q]];
+          lane[l] = s;
+        }
+        y[i] = tree64(lane);
+      }
+    } else {
+      const int32_t i = row0;
+      for (int t = 0; t < TPB; ++t) {
+        double s = 0.0;
+        for (int64_t q = A->rp[i] + t; q < A->rp[i + 1]; q += TPB) s = s + A->v[q] * x[A->ci[q]];
+        acc[t] = s;
+      }
+      y[i] = tree256(acc);
+    }
+  }
+}
+
+static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
+  if (S) spmv_canon(A, S, x, y);
+  else spmv_faithful(A, x, y);
+}
+
+/* ------------------------------------------------------------ dot / norm */
+/* alpha = v . w: device order = per-thread fma accumulators over the item walk. */
+static double dot_canon(const osched* S, const double* v, const double* w, double* P) {
+  double acc[TPB];
+  for (int b = 0; b < S->G; ++b) {
+    for (int t = 0; t < TPB; ++t) acc[t] = 0.0;
+    for (int32_t it = b; it < S->n_items; it += S->G) {
+      const int32_t* I = S->items + 4 * it;
+      const int32_t row0 = I[0], row1 = I[1], kind = I[3];
+      if (kind == 0) {
+        for (int t = 0; t < TPB; ++t)
+          for (int32_t i = row0 + t; i < row1; i += TPB) acc[t] = fma(v[i], w[i], acc[t]);
+      } else if (kind == 1) {
+        for (int32_t i = row0; i < row1; ++i) {
+          const int t = 64 * (i - row0);
+          acc[t] = fma(v[i], w[i], acc[t]);
+        }
+      } else {
+        acc[0] = fma(v[row0], w[row0], acc[0]);
+      }
+    }
+    P[b] = tree256(acc);
+  }
+  return reduce_partials(P, S->G);
+}
+static double dot_faithful(int64_t n, const double* v, const double* w) {
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s = s + v[i] * w[i];
+  return s;
+}
+
+/* ||x||^2: device order = E-partition, thread t visits pairs bE + 2t + 512q. */
+static double nrm2_canon(const osched* S, int64_t n, const double* x, double* P) {
+  double acc[TPB];
+  for (int b = 0; b < S->G; ++b) {
+    const int64_t beg = (int64_t)b * S->E;
+    const int64_t end = beg + S->E < n ? beg + S->E : n;
+    for (int t = 0; t < TPB; ++t) {
+      double a = 0.0;
+      for (int64_t i0 = beg + 2 * t; i0 < end; i0 += 2 * TPB) {
+        a = fma(x[i0], x[i0], a);
+        if (i0 + 1 < end) a = fma(x[i0 + 1], x[i0 + 1], a);
+      }
+      acc[t] = a;
+    }
+    P[b] = tree256(acc);
+  }
+  return reduce_partials(P, S->G);
+}
+static double nrm2_faithful(int64_t n, const double* x) {
+  double s = 0.0;
+  for (int64_t i = 0; i < n; ++i) s = s + x[i] * x[i];
+  return s;
+}
+
+/* ------------------------------------------------------------ drivers */
+/* Standard / pass one. V (n x k, column-major) may be NULL (pass one). */
+int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, double* alphas,
+                    double* betas, size_t* steps, double* bnorm_out, double* V) {
+  const int64_t n = A->n;
+  if (k == 0) return OR_BAD;
+  double* P = S ? (double*)malloc(sizeof(double) * (S->G > 0 ? S->G : 1)) : NULL;
+  double* vp = (double*)calloc((size_t)n + 1, sizeof(double));
+  double* vc = (double*)malloc(sizeof(double) * ((size_t)n + 1));
+  double* w = (double*)malloc(sizeof(double) * ((size_t)n + 1));
+  const double bnorm = sqrt(S ? nrm2_canon(S, n, b, P) : nrm2_faithful(n, b));
+  *bnorm_out = bnorm;
+  *steps = 0;
+  if (bnorm <= TOL) { /* src/algorithms/mod.rs:267-273 */
+    free(P); free(vp); free(vc); free(w);
+    return OR_ZERO_B;
+  }
+  const double inv0 = 1.0 / bnorm;
+  for (int64_t i = 0; i < n; ++i) vc[i] = b[i] * inv0;
+  double beta_prev = 0.0;
+  size_t nb = 0;
+  for (size_t it = 0; it < k; ++it) {
+    if (V) memcpy(V + it * (size_t)n, vc, sizeof(double) * (size_t)n);
+    spmv(A, S, vc, w);                                                /* :177 */
+    for (int64_t i = 0; i < n; ++i) w[i] = w[i] - beta_prev * vp[i]; /* :184-186 */
+    const double alpha = S ? dot_canon(S, vc, w, P) : dot_faithful(n, vc, w); /* :191 */
+    alphas[it] = alpha;
+    *steps = it + 1;
+    if (it + 1 == k) break; /* beta_k is never used */
+    for (int64_t i = 0; i < n; ++i) w[i] = w[i] - alpha * vc[i];     /* :196-198 */
+    const double beta = sqrt(S ? nrm2_canon(S, n, w, P) : nrm2_faithful(n, w)); /* :202 */
+    if (beta <= TOL) break;                                           /* :206-208 */
+    betas[nb++] = beta;
+    const double inv = 1.0 / beta;                                    /* :312-315 */
+    for (int64_t i = 0; i < n; ++i) w[i] = w[i] * inv;
+    double* t = vp;
+    vp = vc;
+    vc = w;
+    w = t;
+    beta_prev = beta;
+  }
+  free(P); free(vp); free(vc); free(w);
+  return OR_OK;
+}
+
+/* Pass two; y already scaled by ||b||. V (n x steps) may be NULL. */
+int oracle_pass_two(const ocsr* A, const osched* S, const double* b, const double* alphas,
+                    const double* betas, size_t steps, double bnorm, const double* y, double* x,
+                    double* V) {
+  const int64_t n = A->n;
+  if (bnorm <= TOL) return OR_ZERO_B; /* src/algorithms/lanczos_two_pass.rs:229-235 */
+  if (steps == 0) {
+    memset(x, 0, sizeof(double) * (size_t)n);
+    return OR_OK;
+  }
+  double* vp = (double*)calloc((size_t)n + 1, sizeof(double));
+  double* vc = (double*)malloc(sizeof(double) * ((size_t)n + 1));
+  double* w = (double*)malloc(sizeof(double) * ((size_t)n + 1));
+  const double inv0 = 1.0 / bnorm;
+  for (int64_t i = 0; i < n; ++i) vc[i] = b[i] * inv0;
+  for (int64_t i = 0; i < n; ++i) x[i] = vc[i] * y[0];
+  if (V) memcpy(V, vc, sizeof(double) * (size_t)n);
+  for (size_t j = 0; j + 1 < steps; ++j) {
+    const double alpha = alphas[j], beta = betas[j], beta_prev = j == 0 ? 0.0 : betas[j - 1];
+    spmv(A, S, vc, w);
+    for (int64_t i = 0; i < n; ++i) w[i] = w[i] - beta_prev * vp[i];
+    for (int64_t i = 0; i < n; ++i) w[i] = w[i] - alpha * vc[i];
+    const double inv = 1.0 / beta;
+    for (int64_t i = 0; i < n; ++i) w[i] = w[i] * inv;
+    const double c = y[j + 1];
+    for (int64_t i = 0; i < n; ++i) x[i] = x[i] + c * w[i];
+    double* t = vp;
+    vp = vc;
+    vc = w;
+    w = t;
+    if (V) memcpy(V + (j + 1) * (size_t)n, vc, sizeof(double) * (size_t)n);
+  }
+  free(vp); free(vc); free(w);
+  return OR_OK;
+}
+
+/* x = ||b|| (V y'): canonical = per row fma chain over columns, then scale. */
+void oracle_gemv_recon(int64_t n, size_t steps, const double* V, const double* yprime,
+                       double bnorm, double* x, int canonical) {
+  for (int64_t i = 0; i < n; ++i) {
+    double s = 0.0;
+    if (canonical)
+      for (size_t c = 0; c < steps; ++c) s = fma(V[c * (size_t)n + i], yprime[c], s);
+    else
+      for (size_t c = 0; c < steps; ++c) s = s + V[c * (size_t)n + i] * yprime[c];
+    x[i] = bnorm * s;
+  }
+}
+
+void oracle_spmv(const ocsr* A, const osched* S, const double* x, double* y) { spmv(A, S, x, y); }
+
+double oracle_nrm2(const osched* S, int64_t n, const double* x) {
+  if (!S) return sqrt(nrm2_faithful(n, x));
+  double* P = (double*)malloc(sizeof(double) * (S->G > 0 ? S->G : 1));
+  const double r = sqrt(nrm2_canon(S, n, x, P));
+  free(P);
+  return r;
+}

@@ -1,0 +1,115 @@
+"""Shared test setup.
+
+Marker ``gpu``: needs an MI355X (run with ``-m gpu``); everything else runs on CPU.
+"""
+import hashlib
+import lzma
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "two-pass-lanczos_amd")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+KKT_DIR = os.path.join(GOLDEN, "kkt")
+REF_RESULTS = os.path.join(GOLDEN, "reference_results")
+
+# md5 of the decompressed netgen .dmx files (regenerated from the reference's own
+# netgen sources + recorded .par seeds; tests/golden/make_fixtures.py)
+KKT_MD5 = {
+    5000: "b227b77b86336c8feba472d62304a499",
+    50000: "d3724d6d6ea2d393f640ff07801d5deb",
+    500000: "0266d4c66c21f949db1ac54883378c25",
+}
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: test needs an AMD MI355X (gfx950) GPU")
+
+
+def kkt_paths(arcs: int, tmpdir: str):
+    """(dmx.xz path, 3-line qfc path) for a committed netgen instance."""
+    from tpl_amd.utils.data_loader import write_qfc_3line
+    dmx = os.path.join(KKT_DIR, f"netgen-{arcs}-3.dmx.xz")
+    qfc = os.path.join(tmpdir, f"netgen-{arcs}-3.qfc")
+    if not os.path.exists(qfc):
+        write_qfc_3line(qfc, arcs)
+    return dmx, qfc
+
+
+_KKT_CACHE = {}
+
+
+def load_kkt(arcs: int, tmpdir: str):
+    if arcs not in _KKT_CACHE:
+        from tpl_amd.utils.data_loader import load_kkt_system
+        dmx, qfc = kkt_paths(arcs, tmpdir)
+        _KKT_CACHE[arcs] = load_kkt_system(dmx, qfc)
+    return _KKT_CACHE[arcs]
+
+
+def harness_b(a):
+    """b = A (1/sqrt(n)) 1, as src/bin/tradeoff.rs:235-236 (row-sequential sums)."""
+    n = a.shape[0]
+    x_true = np.full(n, 1.0 / np.sqrt(n))
+    return a @ x_true
+
+
+@pytest.fixture(scope="session")
+def kkt_tmp(tmp_path_factory):
+    return str(tmp_path_factory.mktemp("kkt"))
+
+
+@pytest.fixture(scope="session")
+def kkt5k(kkt_tmp):
+    return load_kkt(5000, kkt_tmp)
+
+
+@pytest.fixture(scope="session")
+def kkt50k(kkt_tmp):
+    return load_kkt(50000, kkt_tmp)
+
+
+def md5_of_xz(path):
+    h = hashlib.md5()
+    with lzma.open(path, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def canon_schedule(a, stream_row_max=32, nnz_cap=2048, rows_cap=1024, wave_row_max=4096,
+                   max_groups=1024):
+    """The device's item schedule rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp,
+    build_items) restated, for oracle runs without a GPU. The GPU tests take the
+    schedule from the live operator instead (HipCsrOp.schedule())."""
+    rp = a.indptr
+    n = a.shape[0]
+    items = []
+    i = 0
+    while i < n:
+        L = rp[i + 1] - rp[i]
+        if L <= stream_row_max:
+            r0, nz0, rows = i, rp[i], 0
+            while (i < n and rp[i + 1] - rp[i] <= stream_row_max and rp[i + 1] - nz0 <= nnz_cap
+                   and rows < rows_cap):
+                i += 1
+                rows += 1
+            items.append([r0, i, nz0, 0])
+        elif L <= wave_row_max:
+            r0 = i
+            while i < n and i - r0 < 4 and stream_row_max < rp[i + 1] - rp[i] <= wave_row_max:
+                i += 1
+            items.append([r0, i, rp[r0], 1])
+        else:
+            items.append([i, i + 1, rp[i], 2])
+            i += 1
+    G = max(1, min(max_groups, len(items)))
+    per = -(-n // G)
+    E = max(512, (per + 511) // 512 * 512)
+    return np.array(items, dtype=np.int32).reshape(-1, 4), G, E

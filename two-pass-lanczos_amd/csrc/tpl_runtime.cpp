@@ -1,0 +1,831 @@
+// tpl_runtime.cpp — operator lifetime, SpMV schedule, and the device-resident
+// Lanczos drivers behind the C ABI (include/tpl.h).
+//
+// The Lanczos loops of the reference (src/algorithms/lanczos.rs:86-128,
+// src/algorithms/lanczos_two_pass.rs:84-102 and :266-309) run entirely on the GPU:
+// the per-step launches are captured once per (variant, k) into a hipGraph and
+// replayed, alpha/beta never leave HBM during a pass, and breakdown is handled
+// on the device (a stop flag turns the remaining launches into no-ops). The only
+// host round trip of a solve is the f(T_k) call between the passes, exactly
+// where the reference calls its closure (src/solvers.rs:71-75, :155-156).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "tpl_device.h"
+#include "tpl_internal.h"
+
+namespace tpl {
+namespace launch {
+hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
+hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s);
+hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
+                   double* W, double* Vcol, int j, hipStream_t s);
+hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
+                   double* r_next, int j, int k, hipStream_t s);
+hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
+                   double* Vcol, hipStream_t s);
+hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
+                   double* v_next, double* x, double* Vcol, int j, hipStream_t s);
+hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
+                      hipStream_t s);
+hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
+                      int64_t E, hipStream_t s);
+hipError_t reorth_reduce(int cols, const double* P, int G, double* h, hipStream_t s);
+hipError_t reorth_update(int64_t n, int cols, const double* V, double* r, const double* h,
+                         double* Pnorm, int G, int64_t E, hipStream_t s);
+} // namespace launch
+
+// ----------------------------------------------------------------- errors
+static thread_local std::string g_last_error;
+void set_last_error(const std::string& m) { g_last_error = m; }
+
+std::string msg_input(const std::string& what) { return "Invalid input parameter: " + what; }
+std::string msg_param_mismatch(const std::string& name, size_t expected, size_t actual) {
+  return "Parameter mismatch: `" + name + "` expects size " + std::to_string(expected) +
+         ", but got " + std::to_string(actual) + ".";
+}
+std::string msg_solver(const std::string& e) {
+  return "The user-provided f(T_k) solver failed: " + e;
+}
+std::string msg_dimension(int64_t operator_cols, int64_t vector_rows) {
+  return "Dimension mismatch: operator has " + std::to_string(operator_cols) +
+         " columns but vector has " + std::to_string(vector_rows) + " rows.";
+}
+std::string msg_evd(const std::string& e) {
+  return "A numerical error occurred during the eigendecomposition of T_k: " + e;
+}
+
+#define HIPCHK(expr)                                                                        \
+  do {                                                                                      \
+    hipError_t e_ = (expr);                                                                 \
+    if (e_ != hipSuccess)                                                                   \
+      ::tpl::fail(e_ == hipErrorOutOfMemory ? TPL_ERR_OUT_OF_MEMORY : TPL_ERR_DEVICE,       \
+                  std::string(#expr) + ": " + hipGetErrorString(e_));                       \
+  } while (0)
+
+template <class F>
+static tpl_status guarded(F&& f) {
+  try {
+    f();
+    g_last_error.clear();
+    return TPL_OK;
+  } catch (const Error& e) {
+    g_last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    g_last_error = "host allocation failed";
+    return TPL_ERR_OUT_OF_MEMORY;
+  } catch (const std::exception& e) {
+    g_last_error = e.what();
+    return TPL_ERR_INVALID_ARGUMENT;
+  }
+}
+
+// ------------------------------------------------------------ schedule
+struct SchedParams {
+  int stream_nnz_cap = kStreamNnzCap;
+  int stream_rows_cap = kStreamRowsCap;
+  int stream_row_max = 32;   // rows longer than this leave STREAM mode
+  int wave_row_max = 4096;   // rows longer than this get a whole workgroup
+  int max_groups = 1024;     // G upper bound (== number of reduction partials)
+};
+
+static std::vector<Item> build_items(int64_t n, const std::vector<int32_t>& rp,
+                                     const SchedParams& sp) {
+  std::vector<Item> items;
+  int64_t i = 0;
+  auto len = [&](int64_t r) { return (int64_t)rp[r + 1] - rp[r]; };
+  while (i < n) {
+    const int64_t L = len(i);
+    if (L <= sp.stream_row_max) {
+      const int64_t row0 = i, nz0 = rp[i];
+      int rows = 0;
+      while (i < n && len(i) <= sp.stream_row_max && (int64_t)rp[i + 1] - nz0 <= sp.stream_nnz_cap &&
+             rows < sp.stream_rows_cap) {
+        ++i;
+        ++rows;
+      }
+      items.push_back(Item{(int32_t)row0, (int32_t)i, (int32_t)nz0, kItemStream});
+    } else if (L <= sp.wave_row_max) {
+      const int64_t row0 = i;
+      int rows = 0;
+      while (i < n && rows < kWaveRowsPerItem && len(i) > sp.stream_row_max &&
+             len(i) <= sp.wave_row_max) {
+        ++i;
+        ++rows;
+      }
+      items.push_back(Item{(int32_t)row0, (int32_t)i, rp[row0], kItemWave});
+    } else {
+      items.push_back(Item{(int32_t)i, (int32_t)(i + 1), rp[i], kItemBlock});
+      ++i;
+    }
+  }
+  return items;
+}
+
+} // namespace tpl
+
+using namespace tpl;
+
+// ---------------------------------------------------------------- objects
+struct tpl_ctx_s {
+  int device = 0;
+  hipStream_t stream = nullptr;
+};
+
+namespace {
+enum GraphKind { kGPass1 = 0, kGStandard = 1, kGPass2 = 2 };
+}
+
+struct tpl_op_s {
+  tpl_ctx_s* ctx = nullptr;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int64_t n = 0, nnz = 0;
+  std::vector<int32_t> h_rowptr;
+  int32_t* d_rowptr = nullptr;
+  int32_t* d_col = nullptr;
+  double* d_val = nullptr;
+  SchedParams sp;
+  std::vector<Item> items;
+  Item* d_items = nullptr;
+  int G = 1;
+  int64_t E = 512;
+  // vectors: b, R0..R2, W, x, V2_0..V2_2, tmp (n each, padded)
+  double* d_vecs = nullptr;
+  int64_t ld = 0;
+  double *b = nullptr, *R[3] = {nullptr, nullptr, nullptr}, *W = nullptr, *x = nullptr,
+         *V2[3] = {nullptr, nullptr, nullptr}, *tmp = nullptr;
+  // solver state
+  size_t kcap = 0;
+  void* d_state = nullptr;  // flags | norms | alphas | betas | y | Pa | Pb | Pr
+  void* h_state = nullptr;  // pinned mirror of flags | norms | alphas | betas
+  DevState S{};
+  double* d_Pr = nullptr;   // reorthogonalisation partials (G * kcap)
+  double* d_V = nullptr;    // standard-variant basis (n x vcols, ld = n)
+  size_t vcols = 0;
+  std::map<std::pair<int, size_t>, hipGraphExec_t> graphs;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+namespace {
+
+bool use_graphs() {
+  const char* e = std::getenv("TPL_NO_GRAPH");
+  return !(e && e[0] == '1');
+}
+
+CsrDev csr_dev(const tpl_op_s* op) {
+  CsrDev A;
+  A.row_ptr = op->d_rowptr;
+  A.col = op->d_col;
+  A.val = op->d_val;
+  A.items = op->d_items;
+  A.n_items = (int32_t)op->items.size();
+  A.G = op->G;
+  A.n = op->n;
+  A.E = op->E;
+  return A;
+}
+
+void drop_graphs(tpl_op_s* op) {
+  for (auto& kv : op->graphs) hipGraphExecDestroy(kv.second);
+  op->graphs.clear();
+}
+
+void rebuild_schedule(tpl_op_s* op) {
+  op->items = build_items(op->n, op->h_rowptr, op->sp);
+  const int64_t ni = (int64_t)op->items.size();
+  op->G = (int)std::max<int64_t>(1, std::min<int64_t>(op->sp.max_groups, ni));
+  const int64_t per = (op->n + op->G - 1) / op->G;
+  op->E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
+  if (op->d_items) HIPCHK(hipFree(op->d_items));
+  op->d_items = nullptr;
+  if (ni > 0) {
+    HIPCHK(hipMalloc(&op->d_items, ni * sizeof(Item)));
+    HIPCHK(hipMemcpy(op->d_items, op->items.data(), ni * sizeof(Item), hipMemcpyHostToDevice));
+  }
+  drop_graphs(op);
+  // partial buffers depend on G: force state reallocation
+  op->kcap = 0;
+}
+
+// state layout: [flags: 4 int32 (16 B)] [norms kcap+1] [alphas kcap] [betas kcap] [y kcap] [Pa G] [Pb G] [Pr G*kcap]
+void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
+  if (k > op->kcap) {
+    const size_t kc = std::max<size_t>(k, 16);
+    drop_graphs(op);
+    if (op->d_state) HIPCHK(hipFree(op->d_state));
+    if (op->h_state) HIPCHK(hipHostFree(op->h_state));
+    if (op->d_Pr) HIPCHK(hipFree(op->d_Pr));
+    op->d_state = nullptr;
+    op->h_state = nullptr;
+    op->d_Pr = nullptr;
+    const size_t doubles = (kc + 1) + 3 * kc + 2 * (size_t)op->G;
+    const size_t bytes = 16 + doubles * sizeof(double);
+    HIPCHK(hipMalloc(&op->d_state, bytes));
+    HIPCHK(hipMemset(op->d_state, 0, bytes));
+    HIPCHK(hipHostMalloc(&op->h_state, 16 + (4 * kc + 1) * sizeof(double), hipHostMallocDefault));
+    char* base = (char*)op->d_state;
+    op->S.flags = (int32_t*)base;
+    op->S.norms = (double*)(base + 16);
+    op->S.alphas = op->S.norms + (kc + 1);
+    op->S.betas = op->S.alphas + kc;
+    op->S.y = op->S.betas + kc;
+    op->S.Pa = op->S.y + kc;
+    op->S.Pb = op->S.Pa + op->G;
+    op->kcap = kc;
+  }
+  if (reorth && !op->d_Pr) {
+    // [cols x G partials][cols coefficients]
+    HIPCHK(hipMalloc(&op->d_Pr, ((size_t)op->G + 1) * op->kcap * sizeof(double)));
+  }
+}
+
+void ensure_basis(tpl_op_s* op, size_t cols) {
+  if (cols <= op->vcols && op->d_V) return;
+  drop_graphs(op);
+  if (op->d_V) HIPCHK(hipFree(op->d_V));
+  op->d_V = nullptr;
+  op->vcols = 0;
+  const size_t c = std::max<size_t>(cols, 1);
+  HIPCHK(hipMalloc(&op->d_V, (size_t)op->n * c * sizeof(double) + 64));
+  op->vcols = c;
+}
+
+void set_device(const tpl_op_s* op) { HIPCHK(hipSetDevice(op->device)); }
+
+void check_b(const tpl_op_s* op, const double* b, int64_t b_len) {
+  if (!b && op->n > 0) fail(TPL_ERR_INVALID_ARGUMENT, "b is NULL");
+  if (b_len != op->n) fail(TPL_ERR_DIMENSION_MISMATCH, msg_dimension(op->n, b_len));
+}
+
+void upload_vec(tpl_op_s* op, double* dst, const double* src, int mem) {
+  if (op->n == 0) return;
+  HIPCHK(hipMemcpyAsync(dst, src, op->n * sizeof(double),
+                        mem == TPL_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                        op->stream));
+}
+void download_vec(tpl_op_s* op, double* dst, const double* src, int64_t count, int mem) {
+  if (count == 0) return;
+  HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(double),
+                        mem == TPL_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                        op->stream));
+}
+
+// r_j buffer of pass one: r_1 = b, then R[j % 3].
+inline const double* r_of(const tpl_op_s* op, int j) { return j == 1 ? op->b : op->R[j % 3]; }
+
+// ---- reorthogonalisation (extension, not in the reference): classical Gram-Schmidt,
+// applied twice, of r_{j+1} against the stored columns V[:, 0..j) before beta_j.
+void enqueue_reorth(tpl_op_s* op, int j) {
+  const int cols = j; // v_1 .. v_j are stored in V[:, 0..j)
+  double* P = op->d_Pr;                                // cols x G partials
+  double* h = op->d_Pr + (size_t)op->G * op->kcap;    // cols coefficients
+  double* r = op->R[(j + 1) % 3];
+  for (int pass = 0; pass < 2; ++pass) {
+    HIPCHK(launch::reorth_dot(op->n, cols, op->d_V, r, P, op->G, op->E, op->stream));
+    HIPCHK(launch::reorth_reduce(cols, P, op->G, h, op->stream));
+    // the second update also rewrites the ||r||^2 partials that k_p1_spmv(j+1) reduces
+    HIPCHK(launch::reorth_update(op->n, cols, op->d_V, r, h, pass == 1 ? op->S.Pb : nullptr,
+                                 op->G, op->E, op->stream));
+  }
+}
+
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
+  const CsrDev A = csr_dev(op);
+  HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
+  for (int j = 1; j <= (int)k; ++j) {
+    double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
+    HIPCHK(launch::p1_spmv(A, op->S, r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr, op->W,
+                           Vcol, j, op->stream));
+    HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, (int)k,
+                           op->stream));
+    if (reorth && j < (int)k) enqueue_reorth(op, j);
+  }
+}
+
+void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
+  const CsrDev A = csr_dev(op);
+  HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, op->stream));
+  for (int j = 1; j < (int)steps; ++j) {
+    double* Vcol = Vout ? Vout + (size_t)j * op->n : nullptr;
+    HIPCHK(launch::p2_spmv(A, op->S, op->V2[j % 3], j >= 2 ? op->V2[(j - 1) % 3] : nullptr,
+                           op->V2[(j + 1) % 3], op->x, Vcol, j, op->stream));
+  }
+}
+
+template <class Enq>
+void run_graph(tpl_op_s* op, int kind, size_t key, Enq&& enqueue) {
+  if (!use_graphs()) {
+    enqueue();
+    return;
+  }
+  auto it = op->graphs.find({kind, key});
+  if (it == op->graphs.end()) {
+    HIPCHK(hipStreamBeginCapture(op->stream, hipStreamCaptureModeThreadLocal));
+    try {
+      enqueue();
+    } catch (...) {
+      hipGraph_t g = nullptr;
+      hipStreamEndCapture(op->stream, &g);
+      if (g) hipGraphDestroy(g);
+      throw;
+    }
+    hipGraph_t g = nullptr;
+    HIPCHK(hipStreamEndCapture(op->stream, &g));
+    hipGraphExec_t ge = nullptr;
+    hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    HIPCHK(e);
+    it = op->graphs.emplace(std::make_pair(kind, key), ge).first;
+  }
+  HIPCHK(hipGraphLaunch(it->second, op->stream));
+}
+
+struct HostDecomp {
+  int32_t flags[4];
+  double b_norm;
+  const double* alphas;
+  const double* betas;
+  size_t steps;
+};
+
+// Copy flags | norms[0] | alphas | betas back (one D2H), synchronise.
+HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
+  const size_t kc = op->kcap;
+  char* h = (char*)op->h_state;
+  const size_t bytes = 16 + ((kc + 1) + 2 * kc) * sizeof(double);
+  (void)k;
+  HIPCHK(hipMemcpyAsync(h, op->d_state, bytes, hipMemcpyDeviceToHost, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  HostDecomp d;
+  std::memcpy(d.flags, h, 16);
+  const double* norms = (const double*)(h + 16);
+  d.b_norm = norms[0];
+  d.alphas = norms + (kc + 1);
+  d.betas = d.alphas + kc;
+  d.steps = (size_t)d.flags[2];
+  return d;
+}
+
+void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV, bool reorth) {
+  ensure_state(op, k, reorth);
+  if (storeV) ensure_basis(op, k);
+  upload_vec(op, op->b, b, mem);
+  if (reorth) {
+    enqueue_pass1(op, k, true, true); // eager: reorth launch counts vary with j
+  } else {
+    run_graph(op, storeV ? kGStandard : kGPass1, k, [&] { enqueue_pass1(op, k, storeV, false); });
+  }
+}
+
+void check_k(size_t k) {
+  // The reference panics at k = 0 (Vec::with_capacity(k - 1) underflow,
+  // src/algorithms/lanczos.rs:75); the C ABI reports it instead.
+  if (k == 0) fail(TPL_ERR_INPUT, msg_input("The number of iterations `k` must be at least 1."));
+  if (k > (size_t)INT32_MAX / 2) fail(TPL_ERR_INVALID_ARGUMENT, "k too large");
+}
+
+void call_ftk(tpl_ftk_fn f, void* user, const HostDecomp& d, std::vector<double>& y) {
+  if (!f) fail(TPL_ERR_INVALID_ARGUMENT, "f_tk_solver is NULL");
+  y.assign(d.steps, 0.0);
+  size_t ylen = d.steps;
+  char err[1024];
+  err[0] = '\0';
+  const int rc = f(d.alphas, d.steps, d.betas, d.steps > 0 ? d.steps - 1 : 0, y.data(), d.steps,
+                   &ylen, err, sizeof(err), user);
+  err[sizeof(err) - 1] = '\0';
+  if (rc != 0) fail(TPL_ERR_SOLVER, msg_solver(err));
+  if (ylen != d.steps)
+    fail(TPL_ERR_PARAMETER_MISMATCH, msg_param_mismatch("y_k_prime", d.steps, ylen));
+}
+
+void zero_out(tpl_op_s* op, double* x_out, int mem) {
+  if (op->n == 0) return;
+  if (mem == TPL_MEM_DEVICE) {
+    HIPCHK(hipMemsetAsync(x_out, 0, op->n * sizeof(double), op->stream));
+    HIPCHK(hipStreamSynchronize(op->stream));
+  } else {
+    std::memset(x_out, 0, op->n * sizeof(double));
+  }
+}
+
+} // namespace
+
+// =========================================================== C ABI
+extern "C" {
+
+const char* tpl_last_error(void) { return g_last_error.c_str(); }
+const char* tpl_version(void) { return "tpl_amd 0.1.0 gfx950"; }
+
+int tpl_device_count(void) {
+  int c = 0;
+  if (hipGetDeviceCount(&c) != hipSuccess) return 0;
+  return c;
+}
+
+tpl_status tpl_ctx_create(int device, tpl_ctx_t* out) {
+  return guarded([&] {
+    if (!out) fail(TPL_ERR_INVALID_ARGUMENT, "out is NULL");
+    int cnt = 0;
+    if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0)
+      fail(TPL_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= cnt) fail(TPL_ERR_INVALID_ARGUMENT, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    auto c = std::make_unique<tpl_ctx_s>();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    *out = c.release();
+  });
+}
+
+tpl_status tpl_ctx_destroy(tpl_ctx_t ctx) {
+  return guarded([&] {
+    if (!ctx) return;
+    hipSetDevice(ctx->device);
+    if (ctx->stream) hipStreamDestroy(ctx->stream);
+    delete ctx;
+  });
+}
+
+tpl_status tpl_ctx_synchronize(tpl_ctx_t ctx) {
+  return guarded([&] {
+    if (!ctx) fail(TPL_ERR_INVALID_ARGUMENT, "ctx is NULL");
+    HIPCHK(hipSetDevice(ctx->device));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_t* row_ptr,
+                             const int32_t* col_idx, const double* vals, tpl_op_t* out) {
+  return guarded([&] {
+    if (!ctx || !out) fail(TPL_ERR_INVALID_ARGUMENT, "ctx/out is NULL");
+    if (n < 0 || nnz < 0) fail(TPL_ERR_INVALID_ARGUMENT, "negative size");
+    if (n >= INT32_MAX || nnz >= INT32_MAX)
+      fail(TPL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 (int32 device offsets)");
+    if (!row_ptr) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr is NULL");
+    if (nnz > 0 && (!col_idx || !vals)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    if (row_ptr[0] != 0 || row_ptr[n] != nnz)
+      fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0 and end at nnz");
+    for (int64_t i = 0; i < n; ++i) {
+      if (row_ptr[i + 1] < row_ptr[i]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
+      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+        const int32_t c = col_idx[q];
+        if (c < 0 || c >= n) fail(TPL_ERR_INVALID_ARGUMENT, "column index out of range");
+        if (q > row_ptr[i] && c <= col_idx[q - 1])
+          fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be strictly ascending per row");
+      }
+    }
+    HIPCHK(hipSetDevice(ctx->device));
+    auto op = std::make_unique<tpl_op_s>();
+    op->ctx = ctx;
+    op->device = ctx->device;
+    op->stream = ctx->stream;
+    op->n = n;
+    op->nnz = nnz;
+    op->h_rowptr.resize(n + 1);
+    for (int64_t i = 0; i <= n; ++i) op->h_rowptr[i] = (int32_t)row_ptr[i];
+    HIPCHK(hipMalloc(&op->d_rowptr, (n + 1) * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(op->d_rowptr, op->h_rowptr.data(), (n + 1) * sizeof(int32_t),
+                     hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&op->d_col, std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
+    HIPCHK(hipMalloc(&op->d_val, std::max<int64_t>(nnz, 1) * sizeof(double)));
+    if (nnz > 0) {
+      HIPCHK(hipMemcpy(op->d_col, col_idx, nnz * sizeof(int32_t), hipMemcpyHostToDevice));
+      HIPCHK(hipMemcpy(op->d_val, vals, nnz * sizeof(double), hipMemcpyHostToDevice));
+    }
+    rebuild_schedule(op.get());
+    // vectors: b, R0..2, W, x, V2_0..2, tmp = 10 vectors, each padded to 64 doubles
+    op->ld = ((std::max<int64_t>(n, 1) + 63) / 64) * 64;
+    HIPCHK(hipMalloc(&op->d_vecs, 10 * op->ld * sizeof(double)));
+    HIPCHK(hipMemset(op->d_vecs, 0, 10 * op->ld * sizeof(double)));
+    double* p = op->d_vecs;
+    op->b = p;
+    p += op->ld;
+    for (int i = 0; i < 3; ++i, p += op->ld) op->R[i] = p;
+    op->W = p;
+    p += op->ld;
+    op->x = p;
+    p += op->ld;
+    for (int i = 0; i < 3; ++i, p += op->ld) op->V2[i] = p;
+    op->tmp = p;
+    HIPCHK(hipEventCreate(&op->ev0));
+    HIPCHK(hipEventCreate(&op->ev1));
+    *out = op.release();
+  });
+}
+
+tpl_status tpl_op_destroy(tpl_op_t op) {
+  return guarded([&] {
+    if (!op) return;
+    hipSetDevice(op->device);
+    hipStreamSynchronize(op->stream);
+    drop_graphs(op);
+    hipFree(op->d_rowptr);
+    hipFree(op->d_col);
+    hipFree(op->d_val);
+    if (op->d_items) hipFree(op->d_items);
+    hipFree(op->d_vecs);
+    if (op->d_state) hipFree(op->d_state);
+    if (op->h_state) hipHostFree(op->h_state);
+    if (op->d_Pr) hipFree(op->d_Pr);
+    if (op->d_V) hipFree(op->d_V);
+    if (op->ev0) hipEventDestroy(op->ev0);
+    if (op->ev1) hipEventDestroy(op->ev1);
+    delete op;
+  });
+}
+
+int64_t tpl_op_nrows(tpl_op_t op) { return op ? op->n : -1; }
+int64_t tpl_op_nnz(tpl_op_t op) { return op ? op->nnz : -1; }
+
+tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
+  return guarded([&] {
+    if (!op || ((!x || !y) && op->n > 0)) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    set_device(op);
+    if (op->n == 0) return;
+    upload_vec(op, op->tmp, x, mem);
+    HIPCHK(launch::spmv(csr_dev(op), op->tmp, op->W, op->stream));
+    download_vec(op, y, op->W, op->n, mem);
+    HIPCHK(hipStreamSynchronize(op->stream));
+  });
+}
+
+tpl_status tpl_lanczos_pass_one(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                                double* alphas, double* betas, size_t* steps, double* b_norm,
+                                int mem) {
+  return guarded([&] {
+    if (!op || !alphas || !betas || !steps || !b_norm)
+      fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    set_device(op);
+    check_b(op, b, b_len);
+    check_k(k);
+    run_pass_one(op, b, k, mem, false, false);
+    const HostDecomp d = fetch_decomp(op, k);
+    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    std::memcpy(alphas, d.alphas, d.steps * sizeof(double));
+    if (d.steps > 1) std::memcpy(betas, d.betas, (d.steps - 1) * sizeof(double));
+    *steps = d.steps;
+    *b_norm = d.b_norm;
+  });
+}
+
+tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                                double* alphas, double* betas, size_t* steps, double* b_norm,
+                                double* v_out, int mem, int reorth, tpl_step_cb cb,
+                                void* cb_user) {
+  return guarded([&] {
+    if (!op || !alphas || !betas || !steps || !b_norm)
+      fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    set_device(op);
+    check_b(op, b, b_len);
+    check_k(k);
+    HostDecomp d;
+    if (!cb) {
+      run_pass_one(op, b, k, mem, true, reorth != 0);
+      d = fetch_decomp(op, k);
+    } else {
+      // Slow path mirroring src/algorithms/lanczos.rs:86-128 with a host callback per step.
+      ensure_state(op, k, reorth != 0);
+      ensure_basis(op, k);
+      upload_vec(op, op->b, b, mem);
+      const CsrDev A = csr_dev(op);
+      HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
+      for (int j = 1; j <= (int)k; ++j) {
+        HIPCHK(launch::p1_spmv(A, op->S, r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr, op->W,
+                               op->d_V + (size_t)(j - 1) * op->n, j, op->stream));
+        HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, (int)k,
+                               op->stream));
+        d = fetch_decomp(op, k);
+        if (d.flags[0] || d.steps < (size_t)j) break; // zero b or breakdown before step j
+        const int go = cb((size_t)j, op->d_V, op->n, d.alphas, d.steps, d.betas,
+                          d.steps > 0 ? d.steps - 1 : 0, cb_user);
+        if (!go) break;
+        if (reorth && j < (int)k) enqueue_reorth(op, j);
+      }
+      d = fetch_decomp(op, k);
+    }
+    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    std::memcpy(alphas, d.alphas, d.steps * sizeof(double));
+    if (d.steps > 1) std::memcpy(betas, d.betas, (d.steps - 1) * sizeof(double));
+    *steps = d.steps;
+    *b_norm = d.b_norm;
+    if (v_out && d.steps > 0) {
+      download_vec(op, v_out, op->d_V, (int64_t)d.steps * op->n, mem);
+      HIPCHK(hipStreamSynchronize(op->stream));
+    }
+  });
+}
+
+tpl_status tpl_lanczos_pass_two(tpl_op_t op, const double* b, int64_t b_len, const double* alphas,
+                                size_t n_alphas, const double* betas, size_t n_betas,
+                                size_t steps, double b_norm, const double* y, size_t y_len,
+                                double* x_out, double* v_out, int mem) {
+  return guarded([&] {
+    if (!op || !x_out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    set_device(op);
+    check_b(op, b, b_len);
+    // src/algorithms/lanczos_two_pass.rs:220-227
+    if (steps != y_len) fail(TPL_ERR_PARAMETER_MISMATCH, msg_param_mismatch("y_k", steps, y_len));
+    // :229-235
+    if (b_norm <= kBreakdownTol)
+      fail(TPL_ERR_INPUT, msg_input("The initial vector `b` must not be a zero vector."));
+    if (steps == 0) { // :237-244
+      zero_out(op, x_out, mem);
+      return;
+    }
+    if (n_alphas < steps || n_betas + 1 < steps || !alphas || (steps > 1 && !betas) || !y)
+      fail(TPL_ERR_INVALID_ARGUMENT, "decomposition arrays shorter than steps_taken");
+    ensure_state(op, steps);
+    // decomposition -> device: norms[0], alphas, betas, y
+    std::vector<double> host(1 + 3 * op->kcap, 0.0);
+    (void)host;
+    HIPCHK(hipMemcpyAsync(op->S.norms, &b_norm, sizeof(double), hipMemcpyHostToDevice, op->stream));
+    HIPCHK(hipMemcpyAsync(op->S.alphas, alphas, steps * sizeof(double), hipMemcpyHostToDevice,
+                          op->stream));
+    if (steps > 1)
+      HIPCHK(hipMemcpyAsync(op->S.betas, betas, (steps - 1) * sizeof(double),
+                            hipMemcpyHostToDevice, op->stream));
+    HIPCHK(hipMemcpyAsync(op->S.y, y, steps * sizeof(double), hipMemcpyHostToDevice, op->stream));
+    upload_vec(op, op->b, b, mem);
+    if (v_out) {
+      ensure_basis(op, steps);
+      enqueue_pass2(op, steps, op->d_V);
+    } else {
+      run_graph(op, kGPass2, steps, [&] { enqueue_pass2(op, steps, nullptr); });
+    }
+    download_vec(op, x_out, op->x, op->n, mem);
+    if (v_out) download_vec(op, v_out, op->d_V, (int64_t)steps * op->n, mem);
+    HIPCHK(hipStreamSynchronize(op->stream));
+  });
+}
+
+tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, size_t k,
+                                tpl_ftk_fn f, void* f_user, double* x_out, int mem) {
+  return guarded([&] {
+    if (!op || !x_out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    set_device(op);
+    check_b(op, b, b_len);
+    check_k(k);
+    // 1. pass one (src/solvers.rs:148)
+    run_pass_one(op, b, k, mem, false, false);
+    const HostDecomp d = fetch_decomp(op, k);
+    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    if (d.steps == 0) { // :150-152
+      zero_out(op, x_out, mem);
+      return;
+    }
+    // 2. f(T_k) e_1 on the host (:155-165)
+    std::vector<double> y;
+    call_ftk(f, f_user, d, y);
+    // 3. y = y' * ||b|| (:169)
+    for (auto& v : y) v = v * d.b_norm;
+    HIPCHK(hipMemcpyAsync(op->S.y, y.data(), d.steps * sizeof(double), hipMemcpyHostToDevice,
+                          op->stream));
+    // 4. pass two (:174)
+    run_graph(op, kGPass2, d.steps, [&] { enqueue_pass2(op, d.steps, nullptr); });
+    download_vec(op, x_out, op->x, op->n, mem);
+    HIPCHK(hipStreamSynchronize(op->stream));
+  });
+}
+
+tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tpl_ftk_fn f,
+                       void* f_user, double* x_out, int mem) {
+  return guarded([&] {
+    if (!op || !x_out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    set_device(op);
+    check_b(op, b, b_len);
+    check_k(k);
+    // 1. standard pass, V_k in HBM (src/solvers.rs:61)
+    run_pass_one(op, b, k, mem, true, false);
+    const HostDecomp d = fetch_decomp(op, k);
+    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    if (d.steps == 0) { // :64-66
+      zero_out(op, x_out, mem);
+      return;
+    }
+    // 2. y' = f(T_k) e_1 (:71-85)
+    std::vector<double> y;
+    call_ftk(f, f_user, d, y);
+    HIPCHK(hipMemcpyAsync(op->S.y, y.data(), d.steps * sizeof(double), hipMemcpyHostToDevice,
+                          op->stream));
+    // 3. x = ||b|| V_k y' (:96-104)
+    HIPCHK(launch::gemv_recon(op->n, (int)d.steps, op->S, op->d_V, op->x, op->stream));
+    download_vec(op, x_out, op->x, op->n, mem);
+    HIPCHK(hipStreamSynchronize(op->stream));
+  });
+}
+
+tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_items, int32_t* G, int32_t* E,
+                           int32_t* items_out) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    if (n_items) *n_items = (int32_t)op->items.size();
+    if (G) *G = op->G;
+    if (E) *E = (int32_t)op->E;
+    if (items_out)
+      for (size_t i = 0; i < op->items.size(); ++i) {
+        items_out[4 * i + 0] = op->items[i].row0;
+        items_out[4 * i + 1] = op->items[i].row1;
+        items_out[4 * i + 2] = op->items[i].nz0;
+        items_out[4 * i + 3] = op->items[i].kind;
+      }
+  });
+}
+
+tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t stream_nnz_cap, int32_t stream_rows_cap,
+                               int32_t wave_row_max, int32_t max_groups) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    set_device(op);
+    if (stream_nnz_cap > 0) {
+      if (stream_nnz_cap > kStreamNnzCap) fail(TPL_ERR_INVALID_ARGUMENT, "stream_nnz_cap > 2048");
+      op->sp.stream_nnz_cap = stream_nnz_cap;
+      op->sp.stream_row_max = std::min(op->sp.stream_row_max, stream_nnz_cap);
+    }
+    if (stream_rows_cap > 0) {
+      if (stream_rows_cap > kStreamRowsCap) fail(TPL_ERR_INVALID_ARGUMENT, "stream_rows_cap > 1024");
+      op->sp.stream_rows_cap = stream_rows_cap;
+    }
+    if (wave_row_max > 0) op->sp.wave_row_max = std::max(wave_row_max, op->sp.stream_row_max);
+    if (max_groups > 0) op->sp.max_groups = max_groups;
+    HIPCHK(hipStreamSynchronize(op->stream));
+    rebuild_schedule(op);
+  });
+}
+
+tpl_status tpl_copy_to_host(void* dst, const void* src_device, size_t bytes) {
+  return guarded([&] {
+    if (bytes == 0) return;
+    if (!dst || !src_device) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIPCHK(hipMemcpy(dst, src_device, bytes, hipMemcpyDeviceToHost));
+  });
+}
+
+double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
+  if (!op) return 0.0;
+  const double n = (double)op->n, nnz = (double)op->nnz;
+  const double csr = 12.0 * nnz + 4.0 * (n + 1.0); // fp64 value + int32 column per nnz, int32 row_ptr
+  switch (kernel) {
+    case TPL_KERNEL_SPMV: return csr + 16.0 * n;          // x read once, y written once
+    case TPL_KERNEL_PASS1_SPMV: return csr + 24.0 * n;    // r_j, r_{j-1} read; w written
+    case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;          // w, r_j read; r_{j+1} written
+    case TPL_KERNEL_PASS2_SPMV: return csr + 40.0 * n;    // v_j, v_{j-1}, x read; v_{j+1}, x written
+    default: return 0.0;
+  }
+}
+
+tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us,
+                              double* algo_bytes) {
+  return guarded([&] {
+    if (!op || !avg_us || iters <= 0) fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
+    set_device(op);
+    if (op->kcap < 4) ensure_state(op, 4);
+    const CsrDev A = csr_dev(op);
+    const int big = (int)op->kcap; // j < k: the AXPY kernel does its vector work
+    auto launch_one = [&]() {
+      switch (kernel) {
+        case TPL_KERNEL_SPMV: HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream)); break;
+        case TPL_KERNEL_PASS1_SPMV:
+          HIPCHK(launch::p1_spmv(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
+          break;
+        case TPL_KERNEL_PASS1_AXPY:
+          HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
+          break;
+        case TPL_KERNEL_PASS2_SPMV:
+          HIPCHK(launch::p2_spmv(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr, 2,
+                                 op->stream));
+          break;
+        default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
+      }
+    };
+    // Valid state for repeated launches: flags clear, partials/norms of a real step.
+    HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
+    HIPCHK(launch::p1_spmv(A, op->S, op->b, nullptr, op->W, nullptr, 1, op->stream));
+    HIPCHK(launch::p1_axpy(A, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
+    HIPCHK(hipStreamSynchronize(op->stream));
+    std::vector<double> host_state(4, 1.0);
+    launch_one(); // warm-up
+    HIPCHK(hipEventRecord(op->ev0, op->stream));
+    for (int i = 0; i < iters; ++i) launch_one();
+    HIPCHK(hipEventRecord(op->ev1, op->stream));
+    HIPCHK(hipEventSynchronize(op->ev1));
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, op->ev0, op->ev1));
+    *avg_us = 1000.0 * (double)ms / iters;
+    if (algo_bytes) *algo_bytes = tpl_kernel_algo_bytes(op, kernel);
+  });
+}
+
+} // extern "C"

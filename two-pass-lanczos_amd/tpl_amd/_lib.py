@@ -1,0 +1,124 @@
+"""ctypes binding of libtpl_amd.so (the C ABI declared in include/tpl.h).
+
+The shared library is built in-tree by ``make -C two-pass-lanczos_amd/csrc`` (or
+``__graft_entry__.build()``). There is deliberately NO fallback: if the library is
+missing, importing the package raises, so a GPU run can never silently use a
+CPU path.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import (CFUNCTYPE, POINTER, c_char, c_char_p, c_double, c_int, c_int32,
+                    c_int64, c_size_t, c_void_p)
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtpl_amd.so")
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"tpl_amd: {LIB_PATH} is missing — build it with `make -C two-pass-lanczos_amd/csrc` "
+        "(or __graft_entry__.build()); there is no CPU fallback")
+
+lib = ctypes.CDLL(LIB_PATH)
+
+# status codes (tpl_status)
+TPL_OK = 0
+TPL_ERR_BREAKDOWN = 1
+TPL_ERR_DIMENSION_MISMATCH = 2
+TPL_ERR_INPUT = 3
+TPL_ERR_PARAMETER_MISMATCH = 4
+TPL_ERR_EVD = 5
+TPL_ERR_SOLVER = 6
+TPL_ERR_INVALID_ARGUMENT = 100
+TPL_ERR_DEVICE = 101
+TPL_ERR_OUT_OF_MEMORY = 102
+TPL_ERR_DATA_LOADER = 103
+TPL_ERR_UNSUPPORTED = 104
+
+TPL_MEM_HOST = 0
+TPL_MEM_DEVICE = 1
+
+TPL_KERNEL_PASS1_SPMV = 0
+TPL_KERNEL_PASS1_AXPY = 1
+TPL_KERNEL_PASS2_SPMV = 2
+TPL_KERNEL_SPMV = 3
+
+PD = POINTER(c_double)
+
+FTK_FN = CFUNCTYPE(c_int, PD, c_size_t, PD, c_size_t, PD, c_size_t, POINTER(c_size_t),
+                   POINTER(c_char), c_size_t, c_void_p)
+STEP_CB = CFUNCTYPE(c_int, c_size_t, c_void_p, c_int64, PD, c_size_t, PD, c_size_t, c_void_p)
+
+
+class CsrHost(ctypes.Structure):
+    _fields_ = [("n", c_int64), ("nnz", c_int64), ("num_nodes", c_int64), ("num_arcs", c_int64),
+                ("row_ptr", POINTER(c_int64)), ("col_idx", POINTER(c_int32)),
+                ("vals", PD)]
+
+
+def _sig(name, restype, *argtypes):
+    fn = getattr(lib, name)
+    fn.restype = restype
+    fn.argtypes = list(argtypes)
+    return fn
+
+
+tpl_last_error = _sig("tpl_last_error", c_char_p)
+tpl_version = _sig("tpl_version", c_char_p)
+tpl_device_count = _sig("tpl_device_count", c_int)
+tpl_ctx_create = _sig("tpl_ctx_create", c_int, c_int, POINTER(c_void_p))
+tpl_ctx_destroy = _sig("tpl_ctx_destroy", c_int, c_void_p)
+tpl_ctx_synchronize = _sig("tpl_ctx_synchronize", c_int, c_void_p)
+tpl_op_create_csr = _sig("tpl_op_create_csr", c_int, c_void_p, c_int64, c_int64,
+                         POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p))
+tpl_op_destroy = _sig("tpl_op_destroy", c_int, c_void_p)
+tpl_op_nrows = _sig("tpl_op_nrows", c_int64, c_void_p)
+tpl_op_nnz = _sig("tpl_op_nnz", c_int64, c_void_p)
+tpl_op_apply = _sig("tpl_op_apply", c_int, c_void_p, c_void_p, c_void_p, c_int)
+tpl_lanczos = _sig("tpl_lanczos", c_int, c_void_p, c_void_p, c_int64, c_size_t, c_void_p,
+                   c_void_p, c_void_p, c_int)
+tpl_lanczos_two_pass = _sig("tpl_lanczos_two_pass", c_int, c_void_p, c_void_p, c_int64,
+                            c_size_t, c_void_p, c_void_p, c_void_p, c_int)
+tpl_lanczos_standard = _sig("tpl_lanczos_standard", c_int, c_void_p, c_void_p, c_int64, c_size_t,
+                            PD, PD, POINTER(c_size_t), PD, c_void_p, c_int, c_int, c_void_p,
+                            c_void_p)
+tpl_lanczos_pass_one = _sig("tpl_lanczos_pass_one", c_int, c_void_p, c_void_p, c_int64, c_size_t,
+                            PD, PD, POINTER(c_size_t), PD, c_int)
+tpl_lanczos_pass_two = _sig("tpl_lanczos_pass_two", c_int, c_void_p, c_void_p, c_int64, PD,
+                            c_size_t, PD, c_size_t, c_size_t, c_double, PD, c_size_t, c_void_p,
+                            c_void_p, c_int)
+tpl_load_kkt_system = _sig("tpl_load_kkt_system", c_int, c_char_p, c_char_p, POINTER(CsrHost))
+tpl_csr_host_free = _sig("tpl_csr_host_free", None, POINTER(CsrHost))
+tpl_op_schedule = _sig("tpl_op_schedule", c_int, c_void_p, POINTER(c_int32), POINTER(c_int32),
+                       POINTER(c_int32), POINTER(c_int32))
+tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_int32, c_int32,
+                           c_int32)
+tpl_profile_kernel = _sig("tpl_profile_kernel", c_int, c_void_p, c_int, c_int, PD, PD)
+tpl_kernel_algo_bytes = _sig("tpl_kernel_algo_bytes", c_double, c_void_p, c_int)
+tpl_copy_to_host = _sig("tpl_copy_to_host", c_int, c_void_p, c_void_p, c_size_t)
+
+# built-in f(T_k) solvers: raw C function pointers usable as tpl_ftk_fn
+FTK_INV_PTR = ctypes.cast(lib.tpl_ftk_inv, c_void_p).value
+FTK_EXP_PTR = ctypes.cast(lib.tpl_ftk_exp, c_void_p).value
+FTK_SQ_PTR = ctypes.cast(lib.tpl_ftk_sq, c_void_p).value
+tpl_ftk_inv = _sig("tpl_ftk_inv", c_int, PD, c_size_t, PD, c_size_t, PD, c_size_t,
+                   POINTER(c_size_t), POINTER(c_char), c_size_t, c_void_p)
+tpl_ftk_exp = _sig("tpl_ftk_exp", c_int, PD, c_size_t, PD, c_size_t, PD, c_size_t,
+                   POINTER(c_size_t), POINTER(c_char), c_size_t, c_void_p)
+tpl_ftk_sq = _sig("tpl_ftk_sq", c_int, PD, c_size_t, PD, c_size_t, PD, c_size_t,
+                  POINTER(c_size_t), POINTER(c_char), c_size_t, c_void_p)
+
+# Every symbol include/tpl.h declares (checked by tests/test_boundary.py).
+EXPORTED = [
+    "tpl_last_error", "tpl_version", "tpl_ctx_create", "tpl_ctx_destroy", "tpl_ctx_synchronize",
+    "tpl_device_count", "tpl_op_create_csr", "tpl_op_destroy", "tpl_op_nrows", "tpl_op_nnz",
+    "tpl_op_apply", "tpl_ftk_inv", "tpl_ftk_exp", "tpl_ftk_sq", "tpl_lanczos",
+    "tpl_lanczos_two_pass", "tpl_lanczos_standard", "tpl_lanczos_pass_one",
+    "tpl_lanczos_pass_two", "tpl_load_kkt_system", "tpl_csr_host_free", "tpl_op_schedule",
+    "tpl_op_set_schedule", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
+]
+
+
+def last_error() -> str:
+    m = tpl_last_error()
+    return m.decode("utf-8", "replace") if m else ""

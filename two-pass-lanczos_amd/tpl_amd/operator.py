@@ -1,0 +1,145 @@
+"""Device-resident CSR operator — the MI355X replacement of faer's
+``LinOp<f64>`` for ``SparseColMatRef<usize, f64>`` (used by the reference at
+src/algorithms/mod.rs:177 and src/algorithms/lanczos_two_pass.rs:186).
+
+``HipCsrOp`` uploads the matrix once; every solver call then keeps the whole
+recurrence in HBM. Vectors may be numpy arrays (host) or torch CUDA tensors
+(device, zero-copy through the C ABI's TPL_MEM_DEVICE mode).
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from ctypes import POINTER, byref, c_double, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from .error import TplError, check
+
+_ctx_lock = threading.Lock()
+_contexts: dict[int, int] = {}
+
+
+def device_count() -> int:
+    return int(_lib.tpl_device_count())
+
+
+def context(device: int = 0) -> int:
+    """One HIP stream per device per process (created lazily)."""
+    with _ctx_lock:
+        if device not in _contexts:
+            h = c_void_p()
+            check(_lib.tpl_ctx_create(device, byref(h)))
+            _contexts[device] = h.value
+        return _contexts[device]
+
+
+def _as_csr_arrays(a):
+    """Accept a scipy sparse matrix (CSR/CSC; A symmetric), a KKTSystem, or a
+    (n, row_ptr, col_idx, vals) tuple; return int64/int32/float64 CSR arrays."""
+    if hasattr(a, "a") and hasattr(a, "num_arcs"):  # KKTSystem
+        a = a.a
+    if isinstance(a, tuple):
+        n, rp, ci, v = a
+        return (int(n), np.ascontiguousarray(rp, dtype=np.int64),
+                np.ascontiguousarray(ci, dtype=np.int32), np.ascontiguousarray(v, dtype=np.float64))
+    import scipy.sparse as sp
+    if not sp.issparse(a):
+        a = sp.csr_matrix(np.asarray(a, dtype=np.float64))
+    m = a.tocsr()
+    m.sort_indices()
+    if m.shape[0] != m.shape[1]:
+        raise TplError(_lib.TPL_ERR_INVALID_ARGUMENT, "operator must be square")
+    return (m.shape[0], m.indptr.astype(np.int64), m.indices.astype(np.int32),
+            m.data.astype(np.float64))
+
+
+def _is_torch_cuda(x) -> bool:
+    return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
+
+
+class HipCsrOp:
+    """Symmetric sparse operator resident in the HBM of one MI355X.
+
+    Mirrors ``LinOp``: ``nrows()``, ``ncols()``, ``apply(x)``.
+    """
+
+    def __init__(self, a, device: int = 0):
+        n, rp, ci, v = _as_csr_arrays(a)
+        self.device = device
+        self._ctx = context(device)
+        h = c_void_p()
+        check(_lib.tpl_op_create_csr(
+            self._ctx, n, int(rp[-1]) if n > 0 else 0,
+            rp.ctypes.data_as(POINTER(c_int64)), ci.ctypes.data_as(POINTER(c_int32)),
+            v.ctypes.data_as(POINTER(c_double)), byref(h)))
+        self._op = h.value
+        self._n = n
+        self._nnz = int(rp[-1]) if n > 0 else 0
+
+    # -- LinOp surface -------------------------------------------------------
+    def nrows(self) -> int:
+        return self._n
+
+    def ncols(self) -> int:
+        return self._n
+
+    @property
+    def nnz(self) -> int:
+        return self._nnz
+
+    @property
+    def handle(self) -> int:
+        return self._op
+
+    def apply(self, x):
+        """y = A x (LinOp::apply)."""
+        if _is_torch_cuda(x):
+            import torch
+            xx = x.reshape(-1).contiguous()
+            torch.cuda.synchronize(xx.device)
+            y = torch.empty_like(xx)
+            check(_lib.tpl_op_apply(self._op, xx.data_ptr(), y.data_ptr(), _lib.TPL_MEM_DEVICE))
+            return y
+        xx = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+        y = np.empty_like(xx)
+        check(_lib.tpl_op_apply(self._op, xx.ctypes.data, y.ctypes.data, _lib.TPL_MEM_HOST))
+        return y
+
+    # -- schedule / measurement ------------------------------------------------
+    def schedule(self):
+        """(items[n_items, 4] int32 {row0,row1,nz0,kind}, G, E) of the fused SpMV kernels."""
+        ni, g, e = c_int32(), c_int32(), c_int32()
+        check(_lib.tpl_op_schedule(self._op, byref(ni), byref(g), byref(e), None))
+        items = np.zeros((ni.value, 4), dtype=np.int32)
+        check(_lib.tpl_op_schedule(self._op, byref(ni), byref(g), byref(e),
+                                   items.ctypes.data_as(POINTER(c_int32))))
+        return items, g.value, e.value
+
+    def set_schedule(self, stream_nnz_cap=0, stream_rows_cap=0, wave_row_max=0, max_groups=0):
+        check(_lib.tpl_op_set_schedule(self._op, stream_nnz_cap, stream_rows_cap, wave_row_max,
+                                       max_groups))
+
+    def profile_kernel(self, kernel: int, iters: int = 200):
+        """(avg microseconds per launch, algorithmic bytes per launch) via HIP events."""
+        us, by = c_double(), c_double()
+        check(_lib.tpl_profile_kernel(self._op, kernel, iters, byref(us), byref(by)))
+        return us.value, by.value
+
+    def algo_bytes(self, kernel: int) -> float:
+        return float(_lib.tpl_kernel_algo_bytes(self._op, kernel))
+
+    def close(self):
+        if getattr(self, "_op", None):
+            _lib.tpl_op_destroy(self._op)
+            self._op = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __repr__(self):
+        return f"HipCsrOp(n={self._n}, nnz={self._nnz}, device={self.device})"
