@@ -175,25 +175,28 @@ tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_c
 void tpl_csr_host_free(tpl_csr_host* csr);
 
 /* ---- introspection / measurement ---------------------------------------- */
-/* Schedule of the fused SpMV kernels: G persistent workgroups walk n_items row
- * items (kind 0 = stream rows, 1 = one wave per row, 2 = one block per row);
- * E = elements per workgroup of the element-wise kernels. items_out may be NULL
- * (then only the counts are returned); else 4 int32 per item:
- * {row0, row1, nz0, kind}. The CPU oracle uses this to reproduce the device
- * reduction order bit for bit.                                                 */
-tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_items, int32_t* G, int32_t* E,
-                           int32_t* items_out);
-/* Schedule tuning (before the first solve; rebuilds the item list):
- * stream_nnz_cap <= 2048, stream_rows_cap <= 1024, max_groups >= 1 (0 = default). */
+/* Schedule of the fused SpMV kernels (DESIGN.md "SpMV schedule"): rows with at most
+ * short_row_max nnz are grouped into n_stream STREAM items {row0, row1, nz0, 0}
+ * (one workgroup each); the n_long longer rows (ascending indices) are cut into 8
+ * column slices processed by XCD-local workgroups and summed by a combine kernel.
+ * G2 workgroups of E elements run the element-wise kernels (= #norm partials).
+ * items_out: 4 * n_stream int32 or NULL; long_rows_out: n_long int32 or NULL.
+ * The CPU oracle uses this to reproduce the device reduction order bit for bit.   */
+tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_stream, int32_t* n_long, int32_t* G2,
+                           int64_t* E, int32_t* items_out, int32_t* long_rows_out);
+/* Schedule tuning (before the first solve; rebuilds the schedule; 0 = keep):
+ * stream_nnz_cap <= 2048, stream_rows_cap <= 1024, short_row_max, max_g2.        */
 tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t stream_nnz_cap, int32_t stream_rows_cap,
-                               int32_t wave_row_max, int32_t max_groups);
+                               int32_t short_row_max, int32_t max_g2);
 
 /* Kernel ids for tpl_profile_kernel */
 enum {
-  TPL_KERNEL_PASS1_SPMV = 0, /* fused SpMV + beta-AXPY + alpha partials (pass one) */
-  TPL_KERNEL_PASS1_AXPY = 1, /* alpha-AXPY + ||w||^2 partials (pass one)          */
-  TPL_KERNEL_PASS2_SPMV = 2, /* fused SpMV + both AXPYs + scale + x += y v (pass two) */
-  TPL_KERNEL_SPMV = 3        /* plain y = A x                                      */
+  TPL_KERNEL_PASS1_SPMV = 0,    /* pass one: SpMV + beta-AXPY + alpha partials (short rows), long-row slices */
+  TPL_KERNEL_PASS1_AXPY = 1,    /* pass one: alpha-AXPY + ||w||^2 partials                                   */
+  TPL_KERNEL_PASS2_SPMV = 2,    /* pass two: SpMV + both AXPYs + scale + x += y v (short rows), slices       */
+  TPL_KERNEL_SPMV = 3,          /* plain y = A x (both kernels)                                              */
+  TPL_KERNEL_PASS1_COMBINE = 4, /* pass one: long rows from slice partials + epilogue                        */
+  TPL_KERNEL_PASS2_COMBINE = 5  /* pass two: long rows from slice partials + epilogue                        */
 };
 /* Time `iters` back-to-back launches of one kernel on the operator's stream with
  * HIP events (a warm-up launch first). Returns the average per launch in

@@ -44,11 +44,15 @@ typedef struct {
 } ocsr;
 
 typedef struct {
-  int32_t n_items;
-  const int32_t* items; /* 4 per item: row0, row1, nz0, kind (0 stream, 1 wave, 2 block) */
-  int32_t G;
-  int64_t E;
+  int32_t n_stream;
+  const int32_t* items;  /* 4 per STREAM item: row0, row1, nz0, 0 */
+  int32_t n_long;
+  const int32_t* lrows;  /* long rows (sliced), ascending */
+  int32_t G2;            /* element-wise workgroups == #norm partials */
+  int64_t E;             /* elements per element-wise workgroup */
 } osched;
+
+#define SLICES 8
 
 /* ------------------------------------------------------------ trees */
 static double tree64(double* a) { /* xor butterfly == pairwise (l, l+half) tree */
@@ -82,37 +86,39 @@ static void spmv_faithful(const ocsr* A, const double* x, double* y) {
   }
 }
 
+/* long row: per slice s (columns [n*s/8, n*(s+1)/8)) lane l sums entries
+ * off_s + l + 64q; butterfly64 -> P[s]; y = 0; y += P[s] (s ascending). */
+static double long_row_canon(const ocsr* A, int32_t i, const double* x) {
+  const int64_t n = A->n;
+  int64_t q = A->rp[i];
+  double y = 0.0;
+  for (int s = 0; s < SLICES; ++s) {
+    const int64_t bound = (s + 1 == SLICES) ? INT64_MAX : n * (s + 1) / SLICES;
+    int64_t e = q;
+    while (e < A->rp[i + 1] && A->ci[e] < bound) ++e;
+    if (s + 1 == SLICES) e = A->rp[i + 1];
+    double lane[64];
+    for (int l = 0; l < 64; ++l) {
+      double p = 0.0;
+      for (int64_t k = q + l; k < e; k += 64) p = p + A->v[k] * x[A->ci[k]];
+      lane[l] = p;
+    }
+    y = y + tree64(lane);
+    q = e;
+  }
+  return y;
+}
+
 static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* y) {
-  double acc[TPB];
-  for (int32_t it = 0; it < S->n_items; ++it) {
+  for (int32_t it = 0; it < S->n_stream; ++it) {
     const int32_t* I = S->items + 4 * it;
-    const int32_t row0 = I[0], row1 = I[1], kind = I[3];
-    if (kind == 0) {
-      for (int32_t i = row0; i < row1; ++i) {
-        double s = 0.0;
-        for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
-        y[i] = s;
-      }
-    } else if (kind == 1) {
-      for (int32_t i = row0; i < row1; ++i) {
-        double lane[64];
-        for (int l = 0; l < 64; ++l) {
-          double s = 0.0;
-          for (int64_t q = A->rp[i] + l; q < A->rp[i + 1]; q += 64) s = s + A->v[q] * x[A->ci[q]];
-          lane[l] = s;
-        }
-        y[i] = tree64(lane);
-      }
-    } else {
-      const int32_t i = row0;
-      for (int t = 0; t < TPB; ++t) {
-        double s = 0.0;
-        for (int64_t q = A->rp[i] + t; q < A->rp[i + 1]; q += TPB) s = s + A->v[q] * x[A->ci[q]];
-        acc[t] = s;
-      }
-      y[i] = tree256(acc);
+    for (int32_t i = I[0]; i < I[1]; ++i) {
+      double s = 0.0;
+      for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
+      y[i] = s;
     }
   }
+  for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_canon(A, S->lrows[r], x);
 }
 
 static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
@@ -121,29 +127,28 @@ static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
 }
 
 /* ------------------------------------------------------------ dot / norm */
-/* alpha = v . w: device order = per-thread fma accumulators over the item walk. */
+/* alpha = v . w in device order: STREAM item i -> partial i (thread t owns rows
+ * row0 + t + 256q, fma accumulation, tree256); combine workgroup c -> partial
+ * n_stream + c (thread t owns long row 256c + t); then reduce_partials. */
 static double dot_canon(const osched* S, const double* v, const double* w, double* P) {
   double acc[TPB];
-  for (int b = 0; b < S->G; ++b) {
-    for (int t = 0; t < TPB; ++t) acc[t] = 0.0;
-    for (int32_t it = b; it < S->n_items; it += S->G) {
-      const int32_t* I = S->items + 4 * it;
-      const int32_t row0 = I[0], row1 = I[1], kind = I[3];
-      if (kind == 0) {
-        for (int t = 0; t < TPB; ++t)
-          for (int32_t i = row0 + t; i < row1; i += TPB) acc[t] = fma(v[i], w[i], acc[t]);
-      } else if (kind == 1) {
-        for (int32_t i = row0; i < row1; ++i) {
-          const int t = 64 * (i - row0);
-          acc[t] = fma(v[i], w[i], acc[t]);
-        }
-      } else {
-        acc[0] = fma(v[row0], w[row0], acc[0]);
-      }
+  for (int32_t it = 0; it < S->n_stream; ++it) {
+    const int32_t* I = S->items + 4 * it;
+    for (int t = 0; t < TPB; ++t) {
+      acc[t] = 0.0;
+      for (int32_t i = I[0] + t; i < I[1]; i += TPB) acc[t] = fma(v[i], w[i], acc[t]);
     }
-    P[b] = tree256(acc);
+    P[it] = tree256(acc);
   }
-  return reduce_partials(P, S->G);
+  const int32_t nc = (S->n_long + TPB - 1) / TPB;
+  for (int32_t c = 0; c < nc; ++c) {
+    for (int t = 0; t < TPB; ++t) {
+      const int32_t ri = c * TPB + t;
+      acc[t] = ri < S->n_long ? fma(v[S->lrows[ri]], w[S->lrows[ri]], 0.0) : 0.0;
+    }
+    P[S->n_stream + c] = tree256(acc);
+  }
+  return reduce_partials(P, S->n_stream + nc);
 }
 static double dot_faithful(int64_t n, const double* v, const double* w) {
   double s = 0.0;
@@ -154,7 +159,7 @@ static double dot_faithful(int64_t n, const double* v, const double* w) {
 /* ||x||^2: device order = E-partition, thread t visits pairs bE + 2t + 512q. */
 static double nrm2_canon(const osched* S, int64_t n, const double* x, double* P) {
   double acc[TPB];
-  for (int b = 0; b < S->G; ++b) {
+  for (int b = 0; b < S->G2; ++b) {
     const int64_t beg = (int64_t)b * S->E;
     const int64_t end = beg + S->E < n ? beg + S->E : n;
     for (int t = 0; t < TPB; ++t) {
@@ -167,7 +172,7 @@ static double nrm2_canon(const osched* S, int64_t n, const double* x, double* P)
     }
     P[b] = tree256(acc);
   }
-  return reduce_partials(P, S->G);
+  return reduce_partials(P, S->G2);
 }
 static double nrm2_faithful(int64_t n, const double* x) {
   double s = 0.0;
@@ -181,7 +186,8 @@ int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, d
                     double* betas, size_t* steps, double* bnorm_out, double* V) {
   const int64_t n = A->n;
   if (k == 0) return OR_BAD;
-  double* P = S ? (double*)malloc(sizeof(double) * (S->G > 0 ? S->G : 1)) : NULL;
+  double* P = S ? (double*)malloc(sizeof(double) * (size_t)(S->n_stream + S->n_long + S->G2 + 1))
+                : NULL;
   double* vp = (double*)calloc((size_t)n + 1, sizeof(double));
   double* vc = (double*)malloc(sizeof(double) * ((size_t)n + 1));
   double* w = (double*)malloc(sizeof(double) * ((size_t)n + 1));
@@ -273,7 +279,7 @@ void oracle_spmv(const ocsr* A, const osched* S, const double* x, double* y) { s
 
 double oracle_nrm2(const osched* S, int64_t n, const double* x) {
   if (!S) return sqrt(nrm2_faithful(n, x));
-  double* P = (double*)malloc(sizeof(double) * (S->G > 0 ? S->G : 1));
+  double* P = (double*)malloc(sizeof(double) * (size_t)(S->G2 + 1));
   const double r = sqrt(nrm2_canon(S, n, x, P));
   free(P);
   return r;

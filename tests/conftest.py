@@ -83,33 +83,27 @@ def md5_of_xz(path):
     return h.hexdigest()
 
 
-def canon_schedule(a, stream_row_max=32, nnz_cap=2048, rows_cap=1024, wave_row_max=4096,
-                   max_groups=1024):
-    """The device's item schedule rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp,
-    build_items) restated, for oracle runs without a GPU. The GPU tests take the
+def canon_schedule(a, short_row_max=32, nnz_cap=2048, rows_cap=1024, max_g2=1024):
+    """The device's schedule rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp,
+    build_schedule) restated, for oracle runs without a GPU. The GPU tests take the
     schedule from the live operator instead (HipCsrOp.schedule())."""
     rp = a.indptr
     n = a.shape[0]
-    items = []
+    items, lrows = [], []
     i = 0
     while i < n:
-        L = rp[i + 1] - rp[i]
-        if L <= stream_row_max:
-            r0, nz0, rows = i, rp[i], 0
-            while (i < n and rp[i + 1] - rp[i] <= stream_row_max and rp[i + 1] - nz0 <= nnz_cap
-                   and rows < rows_cap):
-                i += 1
-                rows += 1
-            items.append([r0, i, nz0, 0])
-        elif L <= wave_row_max:
-            r0 = i
-            while i < n and i - r0 < 4 and stream_row_max < rp[i + 1] - rp[i] <= wave_row_max:
-                i += 1
-            items.append([r0, i, rp[r0], 1])
-        else:
-            items.append([i, i + 1, rp[i], 2])
+        if rp[i + 1] - rp[i] > short_row_max:
+            lrows.append(i)
             i += 1
-    G = max(1, min(max_groups, len(items)))
-    per = -(-n // G)
+            continue
+        r0, nz0, rows = i, rp[i], 0
+        while (i < n and rp[i + 1] - rp[i] <= short_row_max and rp[i + 1] - nz0 <= nnz_cap
+               and rows < rows_cap):
+            i += 1
+            rows += 1
+        items.append([r0, i, nz0, 0])
+    g2 = max(1, min(max_g2, -(-n // 1024)))
+    per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)
-    return np.array(items, dtype=np.int32).reshape(-1, 4), G, E
+    return {"items": np.array(items, dtype=np.int32).reshape(-1, 4),
+            "long_rows": np.array(lrows, dtype=np.int32), "G2": g2, "E": E}

@@ -4,26 +4,36 @@
 //     w = A v_j ; w -= beta_{j-1} v_{j-1} ; alpha_j = v_j . w ; w -= alpha_j v_j ;
 //     beta_j = ||w|| ; v_{j+1} = w * (1/beta_j)
 // has two grid-wide dependencies (alpha before the second AXPY, beta before the
-// next SpMV), so pass one runs as two launches per step:
-//   k_p1_spmv  : [reduce beta partials -> beta_{j-1}, breakdown test]
-//                fused SpMV gathering x = r_j * (1/beta_{j-1})  (the normalisation
-//                v_j = w/beta folded into the gather, bit-identical to storing v_j)
-//                epilogue w = y - beta_{j-1} v_{j-1}; alpha partials (v_j . w)
-//   k_p1_axpy  : [reduce alpha partials -> alpha_j]  r_{j+1} = w - alpha_j v_j ;
-//                ||r_{j+1}||^2 partials
-// Pass two (src/algorithms/lanczos_two_pass.rs:176-312) knows every coefficient,
-// so each step is ONE launch (k_p2_spmv): SpMV + both AXPYs + scale + x += y v.
+// next SpMV). Pass one therefore runs per step:
+//   k_p1_spmv     [reduce beta partials -> beta_{j-1}, breakdown test]
+//                 fused SpMV gathering x = r_j * (1/beta_{j-1}) (the normalisation
+//                 v_j = w/beta folded into the gather, bit-identical to storing v_j);
+//                 short rows: full epilogue w = y - beta_{j-1} v_{j-1}, alpha partials;
+//                 long rows: column-slice partials only
+//   k_p1_combine  long rows: y = sum of slice partials, same epilogue, alpha partials
+//   k_p1_axpy     [reduce alpha partials -> alpha_j] r_{j+1} = w - alpha_j v_j ;
+//                 ||r_{j+1}||^2 partials
+// Pass two (src/algorithms/lanczos_two_pass.rs:176-312) knows every coefficient:
+//   k_p2_spmv + k_p2_combine: SpMV + both AXPYs + scale + x += y v.
 //
 // Arithmetic follows the reference op by op (-ffp-contract=off for this file):
 //   sub(w, mul(beta, v)) -> w - beta*v (two roundings), v = w * (1/beta)
-//   (reciprocal then multiply), x = x + y*v. Reductions use a FIXED tree
-//   (tpl_device.h) so results are run-to-run bitwise reproducible and pass two
+//   (reciprocal then multiply), x = x + y*v. Reductions use the FIXED trees of
+//   tpl_device.h, so results are run-to-run bitwise reproducible and pass two
 //   regenerates pass one's basis bit for bit (reference: basis_drift_fro = 0.0,
 //   results/orthogonality_*.csv).
+//
+// Memory-latency structure: every workgroup issues its independent global loads
+// (CSR arrays, row pointers, epilogue vectors, gathers) before it waits on the
+// grid-reduction prologue, so the partial-sum reduction overlaps the HBM/MALL
+// round trips instead of adding to them.
 #include <hip/hip_runtime.h>
 #include "tpl_device.h"
 
 namespace tpl {
+
+constexpr int kNnzPerThread = kStreamNnzCap / kTPB; // 8
+constexpr int kRowsPerThread = kStreamRowsCap / kTPB; // 4
 
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ double wave_sum(double v) {
@@ -48,105 +58,54 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return r;
 }
 
-__device__ __forceinline__ double reduce_partials(const double* __restrict__ P, int G,
-                                                  double* red) {
+// Issue the partial loads (independent) early ...
+struct PartialRegs {
+  double v[8];
+};
+__device__ __forceinline__ void load_partials(const double* __restrict__ P, int N, PartialRegs& r) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) {
+    const int i = threadIdx.x + u * kTPB;
+    r.v[u] = i < N ? P[i] : 0.0;
+  }
+}
+// ... and reduce them later in the canonical order (s = 0; s += P[t + 256q]).
+__device__ __forceinline__ double finish_partials(const double* __restrict__ P, int N,
+                                                  const PartialRegs& r, double* red) {
   double s = 0.0;
-  for (int i = threadIdx.x; i < G; i += kTPB) s = s + P[i];
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if ((int)threadIdx.x + u * kTPB < N) s = s + r.v[u];
+  for (int i = threadIdx.x + 8 * kTPB; i < N; i += kTPB) s = s + P[i]; // N > 2048 (rare)
   return block_sum(s, red);
 }
 
-// --------------------------------------------------------------- SpMV core
-// Walks the item list of workgroup blockIdx.x (items b, b+G, ...) and calls
-// epi(row, rowsum, acc) once per row, on the thread the canonical order assigns.
-template <class Epi>
-__device__ __forceinline__ void spmv_items(const CsrDev& A, const double* __restrict__ xsrc,
-                                           const double xscale, double* prod, double* red,
-                                           double& acc, const Epi& epi) {
-  const int t = threadIdx.x;
-  for (int it = blockIdx.x; it < A.n_items; it += A.G) {
-    const Item item = A.items[it];
-    if (item.kind == kItemStream) {
-      const int nz0 = item.nz0;
-      const int cnt = A.row_ptr[item.row1] - nz0;
-      // Phase 1: coalesced sweep of the item's nnz; gather x; products -> LDS.
-#pragma unroll
-      for (int u = 0; u < kStreamNnzCap / kTPB; ++u) {
-        const int q = t + u * kTPB;
-        if (q < cnt) {
-          const int c = A.col[nz0 + q];
-          const double a = A.val[nz0 + q];
-          prod[q] = a * (xsrc[c] * xscale);
-        }
-      }
-      __syncthreads();
-      // Phase 2: one thread per row, ascending-column sequential sum.
-      for (int i = item.row0 + t; i < item.row1; i += kTPB) {
-        const int b = A.row_ptr[i] - nz0, e = A.row_ptr[i + 1] - nz0;
-        double s = 0.0;
-        for (int q = b; q < e; ++q) s = s + prod[q];
-        epi(i, s, acc);
-      }
-      __syncthreads(); // LDS reuse by the next item
-    } else if (item.kind == kItemWave) {
-      const int w = t >> 6, lane = t & 63;
-      const int i = item.row0 + w;
-      double s = 0.0;
-      if (i < item.row1) {
-        const int e = A.row_ptr[i + 1];
-        int q = A.row_ptr[i] + lane;
-        // 4 independent gathers in flight per lane; adds stay in canonical order.
-        for (; q + 192 < e; q += 256) {
-          const int c0 = A.col[q], c1 = A.col[q + 64], c2 = A.col[q + 128], c3 = A.col[q + 192];
-          const double a0 = A.val[q], a1 = A.val[q + 64], a2 = A.val[q + 128], a3 = A.val[q + 192];
-          const double p0 = a0 * (xsrc[c0] * xscale), p1 = a1 * (xsrc[c1] * xscale);
-          const double p2 = a2 * (xsrc[c2] * xscale), p3 = a3 * (xsrc[c3] * xscale);
-          s = s + p0;
-          s = s + p1;
-          s = s + p2;
-          s = s + p3;
-        }
-        for (; q < e; q += 64) s = s + A.val[q] * (xsrc[A.col[q]] * xscale);
-      }
-      s = wave_sum(s);
-      if (i < item.row1 && lane == 0) epi(i, s, acc);
-    } else { // kItemBlock: one workgroup per row
-      const int i = item.row0;
-      const int e = A.row_ptr[i + 1];
-      double s = 0.0;
-      int q = A.row_ptr[i] + t;
-      for (; q + 3 * kTPB < e; q += 4 * kTPB) {
-        const int c0 = A.col[q], c1 = A.col[q + kTPB], c2 = A.col[q + 2 * kTPB], c3 = A.col[q + 3 * kTPB];
-        const double a0 = A.val[q], a1 = A.val[q + kTPB], a2 = A.val[q + 2 * kTPB], a3 = A.val[q + 3 * kTPB];
-        const double p0 = a0 * (xsrc[c0] * xscale), p1 = a1 * (xsrc[c1] * xscale);
-        const double p2 = a2 * (xsrc[c2] * xscale), p3 = a3 * (xsrc[c3] * xscale);
-        s = s + p0;
-        s = s + p1;
-        s = s + p2;
-        s = s + p3;
-      }
-      for (; q < e; q += kTPB) s = s + A.val[q] * (xsrc[A.col[q]] * xscale);
-      s = block_sum(s, red);
-      if (t == 0) epi(i, s, acc);
-    }
-  }
-}
-
-// ------------------------------------------------------------- epilogues
+// ----------------------------------------------------------- epilogues
+// Each epilogue: pre(i) loads the row's own vector entries (issued early),
+// apply(i, s, pre, acc) finishes the row given its SpMV sum s.
+struct PreNone {};
 struct EpiSpmv {
   double* y;
-  __device__ __forceinline__ void operator()(int i, double s, double&) const { y[i] = s; }
+  __device__ __forceinline__ PreNone pre(int) const { return {}; }
+  __device__ __forceinline__ void apply(int i, double s, const PreNone&, double&) const { y[i] = s; }
 };
 
-// pass one / standard: w = y - beta_{j-1} v_{j-1}; alpha partial v_j . w
+// pass one / standard: w = y - beta_{j-1} v_{j-1}; alpha partial += v_j . w
+struct Pre1 {
+  double rc, rp;
+};
 struct EpiPass1 {
   const double* r_cur;  // r_j (v_j = r_j * invN_cur)
   const double* r_prev; // r_{j-1} or nullptr (j == 1: v_0 = 0)
   double invN_cur, invN_prev, beta_sub;
   double* W;
   double* Vcol;         // standard variant: column j-1 of V_k, else nullptr
-  __device__ __forceinline__ void operator()(int i, double s, double& acc) const {
-    const double v = r_cur[i] * invN_cur;
-    const double vp = r_prev ? r_prev[i] * invN_prev : 0.0;
+  __device__ __forceinline__ Pre1 pre(int i) const {
+    return Pre1{r_cur[i], r_prev ? r_prev[i] : 0.0};
+  }
+  __device__ __forceinline__ void apply(int i, double s, const Pre1& p, double& acc) const {
+    const double v = p.rc * invN_cur;
+    const double vp = r_prev ? p.rp * invN_prev : 0.0;
     const double w = s - beta_sub * vp;
     W[i] = w;
     if (Vcol) Vcol[i] = v;
@@ -155,6 +114,9 @@ struct EpiPass1 {
 };
 
 // pass two: w = (y - beta_{j-1} v_{j-1}) - alpha_j v_j; v_{j+1} = w / beta_j; x += y_{j+1} v_{j+1}
+struct Pre2 {
+  double vc, vp, x;
+};
 struct EpiPass2 {
   const double* v_cur;
   const double* v_prev; // nullptr at j == 1
@@ -162,25 +124,156 @@ struct EpiPass2 {
   double* v_next;
   double* x;
   double* Vcol; // lanczos_pass_two_with_basis: column j of V'_k, else nullptr
-  __device__ __forceinline__ void operator()(int i, double s, double&) const {
-    const double vc = v_cur[i];
-    const double vp = v_prev ? v_prev[i] : 0.0;
-    double w = s - beta_sub * vp;
-    w = w - alpha * vc;
+  __device__ __forceinline__ Pre2 pre(int i) const {
+    return Pre2{v_cur[i], v_prev ? v_prev[i] : 0.0, x[i]};
+  }
+  __device__ __forceinline__ void apply(int i, double s, const Pre2& p, double&) const {
+    double w = s - beta_sub * p.vp;
+    w = w - alpha * p.vc;
     const double vn = w * invb;
     v_next[i] = vn;
-    x[i] = x[i] + ycoef * vn;
+    x[i] = p.x + ycoef * vn;
     if (Vcol) Vcol[i] = vn;
   }
 };
 
+// --------------------------------------------------------------- SpMV pieces
+// A STREAM item: rows [row0,row1) with <= 2048 nnz. `scale_of()` is evaluated after
+// every independent load of the item is in flight (it may reduce grid partials).
+template <class Epi, class ScaleFn>
+__device__ __forceinline__ void stream_item(const CsrDev& A, const Item item,
+                                            const double* __restrict__ xsrc, ScaleFn scale_of,
+                                            const Epi& epi, double* prod, double& acc,
+                                            double& scale_out) {
+  const int t = threadIdx.x;
+  const int nz0 = item.nz0;
+  // row pointers + epilogue inputs of this thread's rows (independent loads)
+  int rb[kRowsPerThread], re[kRowsPerThread];
+  decltype(epi.pre(0)) pr[kRowsPerThread];
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    const int i = item.row0 + t + q * kTPB;
+    if (i < item.row1) {
+      rb[q] = A.row_ptr[i];
+      re[q] = A.row_ptr[i + 1];
+      pr[q] = epi.pre(i);
+    }
+  }
+  const int cnt = A.row_ptr[item.row1] - nz0;
+  // coalesced sweep of the item's nnz + gathers
+  int cc[kNnzPerThread];
+  double aa[kNnzPerThread], xv[kNnzPerThread];
+#pragma unroll
+  for (int u = 0; u < kNnzPerThread; ++u) {
+    const int q = t + u * kTPB;
+    if (q < cnt) {
+      cc[u] = A.col[nz0 + q];
+      aa[u] = A.val[nz0 + q];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < kNnzPerThread; ++u) {
+    const int q = t + u * kTPB;
+    if (q < cnt) xv[u] = xsrc[cc[u]];
+  }
+  const double scale = scale_of(); // may wait on the grid-partials reduction
+  scale_out = scale;
+#pragma unroll
+  for (int u = 0; u < kNnzPerThread; ++u) {
+    const int q = t + u * kTPB;
+    if (q < cnt) prod[q] = aa[u] * (xv[u] * scale);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    const int i = item.row0 + t + q * kTPB;
+    if (i < item.row1) {
+      double s = 0.0;
+      for (int k = rb[q] - nz0; k < re[q] - nz0; ++k) s = s + prod[k];
+      epi.apply(i, s, pr[q], acc);
+    }
+  }
+}
+
+// A SLICE unit: long rows 4g..4g+3 (one per wave), columns of slice s. Writes P[r][s].
+template <class ScaleFn>
+__device__ __forceinline__ void slice_unit(const CsrDev& A, int g, int s,
+                                           const double* __restrict__ xsrc, ScaleFn scale_of) {
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ri = g * kLongRowsPerGroup + w;
+  const bool live = ri < A.n_long;
+  int b = 0, e = 0;
+  if (live) {
+    b = A.loff[ri * (kSlices + 1) + s];
+    e = A.loff[ri * (kSlices + 1) + s + 1];
+  }
+  // first batch of 4 entries per lane issued before the scale is known
+  int q = b + lane;
+  int c[4];
+  double a[4], xv[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    if (q + 64 * u < e) {
+      c[u] = A.col[q + 64 * u];
+      a[u] = A.val[q + 64 * u];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (q + 64 * u < e) xv[u] = xsrc[c[u]];
+  const double scale = scale_of();
+  double acc = 0.0;
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+    if (q + 64 * u < e) acc = acc + a[u] * (xv[u] * scale);
+  for (q += 256; q < e; q += 256) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (q + 64 * u < e) {
+        c[u] = A.col[q + 64 * u];
+        a[u] = A.val[q + 64 * u];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (q + 64 * u < e) xv[u] = xsrc[c[u]];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+      if (q + 64 * u < e) acc = acc + a[u] * (xv[u] * scale);
+  }
+  acc = wave_sum(acc);
+  if (live && lane == 0) A.P[ri * kSlices + s] = acc;
+}
+
+// Long-row sum from its slice partials (canonical: y = 0; y += P[s], s ascending).
+__device__ __forceinline__ double combine_row(const CsrDev& A, int ri) {
+  double p[kSlices];
+#pragma unroll
+  for (int s = 0; s < kSlices; ++s) p[s] = A.P[ri * kSlices + s];
+  double y = 0.0;
+#pragma unroll
+  for (int s = 0; s < kSlices; ++s) y = y + p[s];
+  return y;
+}
+
 // ------------------------------------------------------------------ kernels
+// Grid of every SpMV kernel: [n_slice_blocks slice units][n_stream stream items].
 __global__ __launch_bounds__(kTPB) void k_spmv(CsrDev A, const double* __restrict__ x,
                                                double* __restrict__ y) {
   __shared__ double prod[kStreamNnzCap];
-  __shared__ double red[4];
-  double acc = 0.0;
-  spmv_items(A, x, 1.0, prod, red, acc, EpiSpmv{y});
+  const int b = blockIdx.x;
+  auto one = [] { return 1.0; };
+  if (b < A.n_slice_blocks) {
+    slice_unit(A, b / kSlices, b % kSlices, x, one);
+  } else {
+    double acc = 0.0, sc;
+    stream_item(A, A.items[b - A.n_slice_blocks], x, one, EpiSpmv{y}, prod, acc, sc);
+  }
+}
+
+__global__ __launch_bounds__(kTPB) void k_spmv_combine(CsrDev A, double* __restrict__ y) {
+  const int ri = blockIdx.x * kTPB + threadIdx.x;
+  if (ri < A.n_long) y[A.lrows[ri]] = combine_row(A, ri);
 }
 
 // Pass-one prologue: ||b||^2 partials, reset flags.
@@ -209,6 +302,26 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
   if (threadIdx.x == 0) S.Pb[blockIdx.x] = p;
 }
 
+// beta_{j-1} from the norm partials; block 0 publishes it. Returns false on breakdown.
+__device__ __forceinline__ bool p1_beta(const CsrDev& A, const DevState& S, const PartialRegs& pr,
+                                        double* red, int j, double& beta) {
+  beta = sqrt(finish_partials(S.Pb, A.G2, pr, red)); // beta_{j-1} (||b|| at j = 1)
+  if (beta <= kBreakdownTol) {
+    // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
+    // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed (src/algorithms/lanczos_two_pass.rs:245-249).
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      S.flags[0] = 1;
+      if (j == 1) S.flags[1] = 1;
+    }
+    return false;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    S.norms[j - 1] = beta;
+    if (j >= 2) S.betas[j - 2] = beta;
+  }
+  return true;
+}
+
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1).
 __global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ r_cur,
@@ -218,32 +331,76 @@ __global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
   __shared__ double prod[kStreamNnzCap];
   __shared__ double red[4];
   if (S.flags[0]) return; // stopped (breakdown / zero b) in an earlier launch
-  const double beta = sqrt(reduce_partials(S.Pb, A.G, red)); // beta_{j-1} (||b|| at j = 1)
-  if (beta <= kBreakdownTol) {
-    // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
-    // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed (src/algorithms/lanczos_two_pass.rs:245-249).
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      S.flags[0] = 1;
-      if (j == 1) S.flags[1] = 1;
-    }
+  PartialRegs pr;
+  load_partials(S.Pb, A.G2, pr);
+  const int b = blockIdx.x;
+  bool ok = true;
+  if (b < A.n_slice_blocks) {
+    slice_unit(A, b / kSlices, b % kSlices, r_cur, [&] {
+      double beta;
+      ok = p1_beta(A, S, pr, red, j, beta);
+      return ok ? 1.0 / beta : 0.0;
+    });
     return;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S.norms[j - 1] = beta;
-    if (j >= 2) S.betas[j - 2] = beta;
   }
   EpiPass1 epi;
   epi.r_cur = r_cur;
   epi.r_prev = (j >= 2) ? r_prev : nullptr;
+  epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
+  epi.W = W;
+  epi.Vcol = Vcol;
+  double beta = 0.0;
+  auto scale_fn = [&] {
+    ok = p1_beta(A, S, pr, red, j, beta);
+    return ok ? 1.0 / beta : 0.0;
+  };
+  // The epilogue's scale/beta are only known after scale_fn(); stream_item applies the
+  // epilogue after it, so fill them through a small indirection.
+  struct EpiLate {
+    EpiPass1* e;
+    const double* beta;
+    __device__ __forceinline__ Pre1 pre(int i) const { return e->pre(i); }
+    __device__ __forceinline__ void apply(int i, double s, const Pre1& p, double& acc) const {
+      EpiPass1 f = *e;
+      f.invN_cur = 1.0 / *beta;
+      f.beta_sub = f.r_prev ? *beta : 0.0;
+      f.apply(i, s, p, acc);
+    }
+  };
+  double acc = 0.0, sc;
+  stream_item(A, A.items[b - A.n_slice_blocks], r_cur, scale_fn, EpiLate{&epi, &beta}, prod, acc,
+              sc);
+  if (!ok) return; // uniform: every thread of every workgroup computed the same beta
+  const double p = block_sum(acc, red);
+  if (threadIdx.x == 0) S.Pa[b - A.n_slice_blocks] = p;
+}
+
+// Pass one / standard: long rows from their slice partials, same epilogue.
+__global__ __launch_bounds__(kTPB) void k_p1_combine(CsrDev A, DevState S,
+                                                     const double* __restrict__ r_cur,
+                                                     const double* __restrict__ r_prev,
+                                                     double* __restrict__ W,
+                                                     double* __restrict__ Vcol, int j) {
+  __shared__ double red[4];
+  if (S.flags[0]) return;
+  const int ri = blockIdx.x * kTPB + threadIdx.x;
+  EpiPass1 epi;
+  epi.r_cur = r_cur;
+  epi.r_prev = (j >= 2) ? r_prev : nullptr;
+  const double beta = S.norms[j - 1];
   epi.invN_cur = 1.0 / beta;
   epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
   epi.beta_sub = (j >= 2) ? beta : 0.0;
   epi.W = W;
   epi.Vcol = Vcol;
   double acc = 0.0;
-  spmv_items(A, r_cur, epi.invN_cur, prod, red, acc, epi);
-  const double p = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pa[blockIdx.x] = p;
+  if (ri < A.n_long) {
+    const int r = A.lrows[ri];
+    const Pre1 p = epi.pre(r);
+    epi.apply(r, combine_row(A, ri), p, acc);
+  }
+  const double part = block_sum(acc, red);
+  if (threadIdx.x == 0) S.Pa[A.n_stream + blockIdx.x] = part;
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
@@ -253,20 +410,35 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   double* __restrict__ r_next, int j, int k) {
   __shared__ double red[4];
   if (S.flags[0]) return;
-  const double alpha = reduce_partials(S.Pa, A.G, red);
+  PartialRegs pr;
+  load_partials(S.Pa, A.NA, pr);
+  const int64_t beg = (int64_t)blockIdx.x * A.E;
+  const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
+  const double invN = 1.0 / S.norms[j - 1];
+  // first pair of this thread issued before alpha is known
+  const int64_t i00 = beg + 2 * threadIdx.x;
+  double2 w0 = make_double2(0.0, 0.0), rc0 = make_double2(0.0, 0.0);
+  if (j < k && i00 + 1 < end) {
+    w0 = *reinterpret_cast<const double2*>(W + i00);
+    rc0 = *reinterpret_cast<const double2*>(r_cur + i00);
+  }
+  const double alpha = finish_partials(S.Pa, A.NA, pr, red);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
   }
   if (j == k) return; // beta_k is never used (src/algorithms/lanczos_two_pass.rs:252-254)
-  const double invN = 1.0 / S.norms[j - 1];
-  const int64_t beg = (int64_t)blockIdx.x * A.E;
-  const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
   double acc = 0.0;
-  for (int64_t i0 = beg + 2 * threadIdx.x; i0 < end; i0 += 2 * kTPB) {
+  for (int64_t i0 = i00; i0 < end; i0 += 2 * kTPB) {
     if (i0 + 1 < end) {
-      const double2 w = *reinterpret_cast<const double2*>(W + i0);
-      const double2 rc = *reinterpret_cast<const double2*>(r_cur + i0);
+      double2 w, rc;
+      if (i0 == i00) {
+        w = w0;
+        rc = rc0;
+      } else {
+        w = *reinterpret_cast<const double2*>(W + i0);
+        rc = *reinterpret_cast<const double2*>(r_cur + i0);
+      }
       double2 r;
       r.x = w.x - alpha * (rc.x * invN);
       r.y = w.y - alpha * (rc.y * invN);
@@ -300,15 +472,9 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
   }
 }
 
-// Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x.
-__global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
-                                                  const double* __restrict__ v_cur,
-                                                  const double* __restrict__ v_prev,
-                                                  double* __restrict__ v_next,
-                                                  double* __restrict__ x,
-                                                  double* __restrict__ Vcol, int j) {
-  __shared__ double prod[kStreamNnzCap];
-  __shared__ double red[4];
+__device__ __forceinline__ EpiPass2 p2_epi(const DevState& S, const double* v_cur,
+                                           const double* v_prev, double* v_next, double* x,
+                                           double* Vcol, int j) {
   EpiPass2 epi;
   epi.v_cur = v_cur;
   epi.v_prev = (j >= 2) ? v_prev : nullptr;
@@ -319,8 +485,42 @@ __global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
   epi.v_next = v_next;
   epi.x = x;
   epi.Vcol = Vcol;
+  return epi;
+}
+
+// Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x (short rows; long
+// rows' slice partials).
+__global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
+                                                  const double* __restrict__ v_cur,
+                                                  const double* __restrict__ v_prev,
+                                                  double* __restrict__ v_next,
+                                                  double* __restrict__ x,
+                                                  double* __restrict__ Vcol, int j) {
+  __shared__ double prod[kStreamNnzCap];
+  const int b = blockIdx.x;
+  auto one = [] { return 1.0; };
+  if (b < A.n_slice_blocks) {
+    slice_unit(A, b / kSlices, b % kSlices, v_cur, one);
+    return;
+  }
+  const EpiPass2 epi = p2_epi(S, v_cur, v_prev, v_next, x, Vcol, j);
+  double acc = 0.0, sc;
+  stream_item(A, A.items[b - A.n_slice_blocks], v_cur, one, epi, prod, acc, sc);
+}
+
+__global__ __launch_bounds__(kTPB) void k_p2_combine(CsrDev A, DevState S,
+                                                     const double* __restrict__ v_cur,
+                                                     const double* __restrict__ v_prev,
+                                                     double* __restrict__ v_next,
+                                                     double* __restrict__ x,
+                                                     double* __restrict__ Vcol, int j) {
+  const int ri = blockIdx.x * kTPB + threadIdx.x;
+  if (ri >= A.n_long) return;
+  const EpiPass2 epi = p2_epi(S, v_cur, v_prev, v_next, x, Vcol, j);
+  const int r = A.lrows[ri];
+  const Pre2 p = epi.pre(r);
   double acc = 0.0;
-  spmv_items(A, v_cur, 1.0, prod, red, acc, epi);
+  epi.apply(r, combine_row(A, ri), p, acc);
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
@@ -344,8 +544,8 @@ __global__ __launch_bounds__(kTPB) void k_gemv_recon(int64_t n, int steps, DevSt
 // so every column sweep is a coalesced stream.
 constexpr int kReorthCols = 8; // columns per workgroup in the h = V^T r kernel
 
-// h partials: grid (G, ceil(cols/8)); workgroup (b, g) owns rows [bE, min(n,(b+1)E))
-// and columns [8g, 8g+8). P[c*G + b] = tree256 of the thread accumulators.
+// h partials: grid (G2, ceil(cols/8)); workgroup (b, g) owns rows [bE, min(n,(b+1)E))
+// and columns [8g, 8g+8). P[c*G2 + b] = tree256 of the thread accumulators.
 __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
                                                      const double* __restrict__ V,
                                                      const double* __restrict__ r,
@@ -375,7 +575,10 @@ __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
 __global__ __launch_bounds__(kTPB) void k_reorth_reduce(const double* __restrict__ P, int G,
                                                         double* __restrict__ h) {
   __shared__ double red[4];
-  const double s = reduce_partials(P + (int64_t)blockIdx.x * G, G, red);
+  PartialRegs pr;
+  const double* Pc = P + (int64_t)blockIdx.x * G;
+  load_partials(Pc, G, pr);
+  const double s = finish_partials(Pc, G, pr, red);
   if (threadIdx.x == 0) h[blockIdx.x] = s;
 }
 
@@ -419,23 +622,43 @@ static inline int elem_grid(int64_t n) {
   if (g < 1) g = 1;
   return (int)g;
 }
+static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + A.n_stream; }
 
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s) {
-  hipLaunchKernelGGL(k_spmv, dim3(A.G), dim3(kTPB), 0, s, A, x, y);
+  if (spmv_grid(A) > 0) hipLaunchKernelGGL(k_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, x, y);
+  if (A.n_comb_blocks > 0)
+    hipLaunchKernelGGL(k_spmv_combine, dim3(A.n_comb_blocks), dim3(kTPB), 0, s, A, y);
   return hipGetLastError();
 }
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_init, dim3(A.G), dim3(kTPB), 0, s, A, S, b);
+  hipLaunchKernelGGL(k_p1_init, dim3(A.G2), dim3(kTPB), 0, s, A, S, b);
   return hipGetLastError();
 }
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
                    double* W, double* Vcol, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_spmv, dim3(A.G), dim3(kTPB), 0, s, A, S, r_cur, r_prev, W, Vcol, j);
+  if (spmv_grid(A) > 0)
+    hipLaunchKernelGGL(k_p1_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, r_cur, r_prev, W,
+                       Vcol, j);
+  if (A.n_comb_blocks > 0)
+    hipLaunchKernelGGL(k_p1_combine, dim3(A.n_comb_blocks), dim3(kTPB), 0, s, A, S, r_cur, r_prev,
+                       W, Vcol, j);
+  return hipGetLastError();
+}
+hipError_t p1_spmv_only(const CsrDev& A, const DevState& S, const double* r_cur,
+                        const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
+  hipLaunchKernelGGL(k_p1_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, r_cur, r_prev, W,
+                     Vcol, j);
+  return hipGetLastError();
+}
+hipError_t p1_combine_only(const CsrDev& A, const DevState& S, const double* r_cur,
+                           const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
+  hipLaunchKernelGGL(k_p1_combine, dim3(A.n_comb_blocks > 0 ? A.n_comb_blocks : 1), dim3(kTPB), 0,
+                     s, A, S, r_cur, r_prev, W, Vcol, j);
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_axpy, dim3(A.G), dim3(kTPB), 0, s, A, S, W, r_cur, r_next, j, k);
+  hipLaunchKernelGGL(k_p1_axpy, dim3(A.G2), dim3(kTPB), 0, s, A, S, W, r_cur, r_next, j, k);
   return hipGetLastError();
 }
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
@@ -445,8 +668,26 @@ hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, do
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
                    double* v_next, double* x, double* Vcol, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_p2_spmv, dim3(A.G), dim3(kTPB), 0, s, A, S, v_cur, v_prev, v_next, x,
-                     Vcol, j);
+  if (spmv_grid(A) > 0)
+    hipLaunchKernelGGL(k_p2_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, v_cur, v_prev,
+                       v_next, x, Vcol, j);
+  if (A.n_comb_blocks > 0)
+    hipLaunchKernelGGL(k_p2_combine, dim3(A.n_comb_blocks), dim3(kTPB), 0, s, A, S, v_cur, v_prev,
+                       v_next, x, Vcol, j);
+  return hipGetLastError();
+}
+hipError_t p2_spmv_only(const CsrDev& A, const DevState& S, const double* v_cur,
+                        const double* v_prev, double* v_next, double* x, double* Vcol, int j,
+                        hipStream_t s) {
+  hipLaunchKernelGGL(k_p2_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, v_cur, v_prev, v_next,
+                     x, Vcol, j);
+  return hipGetLastError();
+}
+hipError_t p2_combine_only(const CsrDev& A, const DevState& S, const double* v_cur,
+                           const double* v_prev, double* v_next, double* x, double* Vcol, int j,
+                           hipStream_t s) {
+  hipLaunchKernelGGL(k_p2_combine, dim3(A.n_comb_blocks > 0 ? A.n_comb_blocks : 1), dim3(kTPB), 0,
+                     s, A, S, v_cur, v_prev, v_next, x, Vcol, j);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,

@@ -30,8 +30,18 @@ hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s);
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
                    double* W, double* Vcol, int j, hipStream_t s);
+hipError_t p1_spmv_only(const CsrDev& A, const DevState& S, const double* r_cur,
+                        const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
+hipError_t p1_combine_only(const CsrDev& A, const DevState& S, const double* r_cur,
+                           const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s);
+hipError_t p2_spmv_only(const CsrDev& A, const DevState& S, const double* v_cur,
+                        const double* v_prev, double* v_next, double* x, double* Vcol, int j,
+                        hipStream_t s);
+hipError_t p2_combine_only(const CsrDev& A, const DevState& S, const double* v_cur,
+                           const double* v_prev, double* v_next, double* x, double* Vcol, int j,
+                           hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, hipStream_t s);
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
@@ -95,42 +105,55 @@ static tpl_status guarded(F&& f) {
 struct SchedParams {
   int stream_nnz_cap = kStreamNnzCap;
   int stream_rows_cap = kStreamRowsCap;
-  int stream_row_max = 32;   // rows longer than this leave STREAM mode
-  int wave_row_max = 4096;   // rows longer than this get a whole workgroup
-  int max_groups = 1024;     // G upper bound (== number of reduction partials)
+  int short_row_max = kShortRowMax; // rows longer than this are sliced
+  int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
 };
 
-static std::vector<Item> build_items(int64_t n, const std::vector<int32_t>& rp,
-                                     const SchedParams& sp) {
-  std::vector<Item> items;
-  int64_t i = 0;
+struct Schedule {
+  std::vector<Item> items;      // STREAM items
+  std::vector<int32_t> lrows;   // long rows, ascending
+  std::vector<int32_t> loff;    // n_long x (kSlices + 1)
+  int G2 = 1;
+  int64_t E = 512;
+};
+
+// Short rows -> STREAM items of consecutive short rows; long rows -> sliced units.
+static Schedule build_schedule(int64_t n, const std::vector<int32_t>& rp,
+                               const std::vector<int32_t>& col, const SchedParams& sp) {
+  Schedule S;
   auto len = [&](int64_t r) { return (int64_t)rp[r + 1] - rp[r]; };
+  int64_t i = 0;
   while (i < n) {
-    const int64_t L = len(i);
-    if (L <= sp.stream_row_max) {
-      const int64_t row0 = i, nz0 = rp[i];
-      int rows = 0;
-      while (i < n && len(i) <= sp.stream_row_max && (int64_t)rp[i + 1] - nz0 <= sp.stream_nnz_cap &&
-             rows < sp.stream_rows_cap) {
-        ++i;
-        ++rows;
-      }
-      items.push_back(Item{(int32_t)row0, (int32_t)i, (int32_t)nz0, kItemStream});
-    } else if (L <= sp.wave_row_max) {
-      const int64_t row0 = i;
-      int rows = 0;
-      while (i < n && rows < kWaveRowsPerItem && len(i) > sp.stream_row_max &&
-             len(i) <= sp.wave_row_max) {
-        ++i;
-        ++rows;
-      }
-      items.push_back(Item{(int32_t)row0, (int32_t)i, rp[row0], kItemWave});
-    } else {
-      items.push_back(Item{(int32_t)i, (int32_t)(i + 1), rp[i], kItemBlock});
+    if (len(i) > sp.short_row_max) {
+      S.lrows.push_back((int32_t)i);
       ++i;
+      continue;
+    }
+    const int64_t row0 = i, nz0 = rp[i];
+    int rows = 0;
+    while (i < n && len(i) <= sp.short_row_max && (int64_t)rp[i + 1] - nz0 <= sp.stream_nnz_cap &&
+           rows < sp.stream_rows_cap) {
+      ++i;
+      ++rows;
+    }
+    S.items.push_back(Item{(int32_t)row0, (int32_t)i, (int32_t)nz0, 0});
+  }
+  // slice offsets: first entry of long row r with column >= floor(n * s / kSlices)
+  S.loff.resize(S.lrows.size() * (kSlices + 1));
+  for (size_t r = 0; r < S.lrows.size(); ++r) {
+    const int32_t row = S.lrows[r];
+    int32_t q = rp[row];
+    for (int s = 0; s <= kSlices; ++s) {
+      const int64_t bound = n * s / kSlices;
+      while (q < rp[row + 1] && col[q] < bound) ++q;
+      S.loff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
     }
   }
-  return items;
+  const int64_t g2 = (n + 1023) / 1024;
+  S.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
+  const int64_t per = (n + S.G2 - 1) / S.G2;
+  S.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
+  return S;
 }
 
 } // namespace tpl
@@ -156,11 +179,13 @@ struct tpl_op_s {
   int32_t* d_rowptr = nullptr;
   int32_t* d_col = nullptr;
   double* d_val = nullptr;
+  std::vector<int32_t> h_col;
   SchedParams sp;
-  std::vector<Item> items;
+  Schedule sched;
   Item* d_items = nullptr;
-  int G = 1;
-  int64_t E = 512;
+  int32_t* d_lrows = nullptr;
+  int32_t* d_loff = nullptr;
+  double* d_P = nullptr;
   // vectors: b, R0..R2, W, x, V2_0..V2_2, tmp (n each, padded)
   double* d_vecs = nullptr;
   int64_t ld = 0;
@@ -191,10 +216,17 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.col = op->d_col;
   A.val = op->d_val;
   A.items = op->d_items;
-  A.n_items = (int32_t)op->items.size();
-  A.G = op->G;
+  A.lrows = op->d_lrows;
+  A.loff = op->d_loff;
+  A.P = op->d_P;
+  A.n_stream = (int32_t)op->sched.items.size();
+  A.n_long = (int32_t)op->sched.lrows.size();
+  A.n_slice_blocks = kSlices * ((A.n_long + kLongRowsPerGroup - 1) / kLongRowsPerGroup);
+  A.n_comb_blocks = (A.n_long + kTPB - 1) / kTPB;
+  A.G2 = op->sched.G2;
+  A.NA = A.n_stream + A.n_comb_blocks;
   A.n = op->n;
-  A.E = op->E;
+  A.E = op->sched.E;
   return A;
 }
 
@@ -203,20 +235,26 @@ void drop_graphs(tpl_op_s* op) {
   op->graphs.clear();
 }
 
+template <class T>
+void upload(T** dst, const std::vector<T>& src) {
+  if (*dst) HIPCHK(hipFree(*dst));
+  *dst = nullptr;
+  if (src.empty()) return;
+  HIPCHK(hipMalloc(dst, src.size() * sizeof(T)));
+  HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
+}
+
 void rebuild_schedule(tpl_op_s* op) {
-  op->items = build_items(op->n, op->h_rowptr, op->sp);
-  const int64_t ni = (int64_t)op->items.size();
-  op->G = (int)std::max<int64_t>(1, std::min<int64_t>(op->sp.max_groups, ni));
-  const int64_t per = (op->n + op->G - 1) / op->G;
-  op->E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
-  if (op->d_items) HIPCHK(hipFree(op->d_items));
-  op->d_items = nullptr;
-  if (ni > 0) {
-    HIPCHK(hipMalloc(&op->d_items, ni * sizeof(Item)));
-    HIPCHK(hipMemcpy(op->d_items, op->items.data(), ni * sizeof(Item), hipMemcpyHostToDevice));
-  }
+  op->sched = build_schedule(op->n, op->h_rowptr, op->h_col, op->sp);
+  upload(&op->d_items, op->sched.items);
+  upload(&op->d_lrows, op->sched.lrows);
+  upload(&op->d_loff, op->sched.loff);
+  if (op->d_P) HIPCHK(hipFree(op->d_P));
+  op->d_P = nullptr;
+  if (!op->sched.lrows.empty())
+    HIPCHK(hipMalloc(&op->d_P, op->sched.lrows.size() * kSlices * sizeof(double)));
   drop_graphs(op);
-  // partial buffers depend on G: force state reallocation
+  // partial buffers depend on the schedule: force state reallocation
   op->kcap = 0;
 }
 
@@ -231,7 +269,8 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->d_state = nullptr;
     op->h_state = nullptr;
     op->d_Pr = nullptr;
-    const size_t doubles = (kc + 1) + 3 * kc + 2 * (size_t)op->G;
+    const CsrDev A = csr_dev(op);
+    const size_t doubles = (kc + 1) + 3 * kc + (size_t)std::max(A.NA, 1) + (size_t)A.G2;
     const size_t bytes = 16 + doubles * sizeof(double);
     HIPCHK(hipMalloc(&op->d_state, bytes));
     HIPCHK(hipMemset(op->d_state, 0, bytes));
@@ -243,12 +282,12 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->S.betas = op->S.alphas + kc;
     op->S.y = op->S.betas + kc;
     op->S.Pa = op->S.y + kc;
-    op->S.Pb = op->S.Pa + op->G;
+    op->S.Pb = op->S.Pa + std::max(A.NA, 1);
     op->kcap = kc;
   }
   if (reorth && !op->d_Pr) {
     // [cols x G partials][cols coefficients]
-    HIPCHK(hipMalloc(&op->d_Pr, ((size_t)op->G + 1) * op->kcap * sizeof(double)));
+    HIPCHK(hipMalloc(&op->d_Pr, ((size_t)op->sched.G2 + 1) * op->kcap * sizeof(double)));
   }
 }
 
@@ -290,15 +329,17 @@ inline const double* r_of(const tpl_op_s* op, int j) { return j == 1 ? op->b : o
 // applied twice, of r_{j+1} against the stored columns V[:, 0..j) before beta_j.
 void enqueue_reorth(tpl_op_s* op, int j) {
   const int cols = j; // v_1 .. v_j are stored in V[:, 0..j)
-  double* P = op->d_Pr;                                // cols x G partials
-  double* h = op->d_Pr + (size_t)op->G * op->kcap;    // cols coefficients
+  const int G2 = op->sched.G2;
+  const int64_t E = op->sched.E;
+  double* P = op->d_Pr;                             // cols x G2 partials
+  double* h = op->d_Pr + (size_t)G2 * op->kcap;    // cols coefficients
   double* r = op->R[(j + 1) % 3];
   for (int pass = 0; pass < 2; ++pass) {
-    HIPCHK(launch::reorth_dot(op->n, cols, op->d_V, r, P, op->G, op->E, op->stream));
-    HIPCHK(launch::reorth_reduce(cols, P, op->G, h, op->stream));
+    HIPCHK(launch::reorth_dot(op->n, cols, op->d_V, r, P, G2, E, op->stream));
+    HIPCHK(launch::reorth_reduce(cols, P, G2, h, op->stream));
     // the second update also rewrites the ||r||^2 partials that k_p1_spmv(j+1) reduces
     HIPCHK(launch::reorth_update(op->n, cols, op->d_V, r, h, pass == 1 ? op->S.Pb : nullptr,
-                                 op->G, op->E, op->stream));
+                                 G2, E, op->stream));
   }
 }
 
@@ -496,6 +537,7 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
     op->nnz = nnz;
     op->h_rowptr.resize(n + 1);
     for (int64_t i = 0; i <= n; ++i) op->h_rowptr[i] = (int32_t)row_ptr[i];
+    op->h_col.assign(col_idx, col_idx + nnz);
     HIPCHK(hipMalloc(&op->d_rowptr, (n + 1) * sizeof(int32_t)));
     HIPCHK(hipMemcpy(op->d_rowptr, op->h_rowptr.data(), (n + 1) * sizeof(int32_t),
                      hipMemcpyHostToDevice));
@@ -536,6 +578,9 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipFree(op->d_col);
     hipFree(op->d_val);
     if (op->d_items) hipFree(op->d_items);
+    if (op->d_lrows) hipFree(op->d_lrows);
+    if (op->d_loff) hipFree(op->d_loff);
+    if (op->d_P) hipFree(op->d_P);
     hipFree(op->d_vecs);
     if (op->d_state) hipFree(op->d_state);
     if (op->h_state) hipHostFree(op->h_state);
@@ -727,39 +772,42 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
   });
 }
 
-tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_items, int32_t* G, int32_t* E,
-                           int32_t* items_out) {
+tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_stream, int32_t* n_long, int32_t* G2,
+                           int64_t* E, int32_t* items_out, int32_t* long_rows_out) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
-    if (n_items) *n_items = (int32_t)op->items.size();
-    if (G) *G = op->G;
-    if (E) *E = (int32_t)op->E;
+    const Schedule& S = op->sched;
+    if (n_stream) *n_stream = (int32_t)S.items.size();
+    if (n_long) *n_long = (int32_t)S.lrows.size();
+    if (G2) *G2 = S.G2;
+    if (E) *E = S.E;
     if (items_out)
-      for (size_t i = 0; i < op->items.size(); ++i) {
-        items_out[4 * i + 0] = op->items[i].row0;
-        items_out[4 * i + 1] = op->items[i].row1;
-        items_out[4 * i + 2] = op->items[i].nz0;
-        items_out[4 * i + 3] = op->items[i].kind;
+      for (size_t i = 0; i < S.items.size(); ++i) {
+        items_out[4 * i + 0] = S.items[i].row0;
+        items_out[4 * i + 1] = S.items[i].row1;
+        items_out[4 * i + 2] = S.items[i].nz0;
+        items_out[4 * i + 3] = 0;
       }
+    if (long_rows_out)
+      for (size_t i = 0; i < S.lrows.size(); ++i) long_rows_out[i] = S.lrows[i];
   });
 }
 
 tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t stream_nnz_cap, int32_t stream_rows_cap,
-                               int32_t wave_row_max, int32_t max_groups) {
+                               int32_t short_row_max, int32_t max_g2) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     set_device(op);
     if (stream_nnz_cap > 0) {
       if (stream_nnz_cap > kStreamNnzCap) fail(TPL_ERR_INVALID_ARGUMENT, "stream_nnz_cap > 2048");
       op->sp.stream_nnz_cap = stream_nnz_cap;
-      op->sp.stream_row_max = std::min(op->sp.stream_row_max, stream_nnz_cap);
     }
     if (stream_rows_cap > 0) {
       if (stream_rows_cap > kStreamRowsCap) fail(TPL_ERR_INVALID_ARGUMENT, "stream_rows_cap > 1024");
       op->sp.stream_rows_cap = stream_rows_cap;
     }
-    if (wave_row_max > 0) op->sp.wave_row_max = std::max(wave_row_max, op->sp.stream_row_max);
-    if (max_groups > 0) op->sp.max_groups = max_groups;
+    if (short_row_max > 0) op->sp.short_row_max = std::min(short_row_max, op->sp.stream_nnz_cap);
+    if (max_g2 > 0) op->sp.max_g2 = max_g2;
     HIPCHK(hipStreamSynchronize(op->stream));
     rebuild_schedule(op);
   });
@@ -776,12 +824,18 @@ tpl_status tpl_copy_to_host(void* dst, const void* src_device, size_t bytes) {
 double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
   if (!op) return 0.0;
   const double n = (double)op->n, nnz = (double)op->nnz;
-  const double csr = 12.0 * nnz + 4.0 * (n + 1.0); // fp64 value + int32 column per nnz, int32 row_ptr
+  const double nl = (double)op->sched.lrows.size(), ns = n - nl;
+  // CSR: fp64 value + int32 column per nnz, int32 row_ptr; the gathered vector
+  // counted once (8n), slice metadata 36 B and 8 partials per long row.
+  const double csr = 12.0 * nnz + 4.0 * (n + 1.0);
+  const double slices = nl * (4.0 * (kSlices + 1) + 8.0 * kSlices);
   switch (kernel) {
-    case TPL_KERNEL_SPMV: return csr + 16.0 * n;          // x read once, y written once
-    case TPL_KERNEL_PASS1_SPMV: return csr + 24.0 * n;    // r_j, r_{j-1} read; w written
-    case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;          // w, r_j read; r_{j+1} written
-    case TPL_KERNEL_PASS2_SPMV: return csr + 40.0 * n;    // v_j, v_{j-1}, x read; v_{j+1}, x written
+    case TPL_KERNEL_SPMV: return csr + 8.0 * n + 8.0 * ns + slices;            // x; y (short rows)
+    case TPL_KERNEL_PASS1_SPMV: return csr + 8.0 * n + 16.0 * ns + slices;     // r_j; r_{j-1}, w (short rows)
+    case TPL_KERNEL_PASS1_COMBINE: return nl * (8.0 * kSlices + 4.0 + 24.0);   // partials; r_j, r_{j-1}, w
+    case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;                               // w, r_j read; r_{j+1} written
+    case TPL_KERNEL_PASS2_SPMV: return csr + 8.0 * n + 32.0 * ns + slices;     // v_j; v_{j-1}, x, v_{j+1}, x (short rows)
+    case TPL_KERNEL_PASS2_COMBINE: return nl * (8.0 * kSlices + 4.0 + 40.0);
     default: return 0.0;
   }
 }
@@ -798,14 +852,21 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
       switch (kernel) {
         case TPL_KERNEL_SPMV: HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream)); break;
         case TPL_KERNEL_PASS1_SPMV:
-          HIPCHK(launch::p1_spmv(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
+          HIPCHK(launch::p1_spmv_only(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
+          break;
+        case TPL_KERNEL_PASS1_COMBINE:
+          HIPCHK(launch::p1_combine_only(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
           break;
         case TPL_KERNEL_PASS1_AXPY:
           HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
-          HIPCHK(launch::p2_spmv(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr, 2,
-                                 op->stream));
+          HIPCHK(launch::p2_spmv_only(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr, 2,
+                                      op->stream));
+          break;
+        case TPL_KERNEL_PASS2_COMBINE:
+          HIPCHK(launch::p2_combine_only(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr,
+                                         2, op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }
@@ -815,7 +876,6 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     HIPCHK(launch::p1_spmv(A, op->S, op->b, nullptr, op->W, nullptr, 1, op->stream));
     HIPCHK(launch::p1_axpy(A, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
     HIPCHK(hipStreamSynchronize(op->stream));
-    std::vector<double> host_state(4, 1.0);
     launch_one(); // warm-up
     HIPCHK(hipEventRecord(op->ev0, op->stream));
     for (int i = 0; i < iters; ++i) launch_one();

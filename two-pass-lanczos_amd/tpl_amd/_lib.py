@@ -19,6 +19,16 @@ if not os.path.exists(LIB_PATH):
         f"tpl_amd: {LIB_PATH} is missing — build it with `make -C two-pass-lanczos_amd/csrc` "
         "(or __graft_entry__.build()); there is no CPU fallback")
 
+# PyTorch-ROCm wheels bundle their own libamdhip64 / libhsa-runtime64 (same SONAMEs
+# as /opt/rocm's). Whichever is loaded first wins the SONAME; loading ours first makes
+# torch pull in a SECOND HIP runtime that cannot see the GPU. Importing torch first
+# (when installed) keeps exactly one HIP runtime in the process, shared by torch
+# (device buffers, torch.distributed) and libtpl_amd.so.
+try:  # pragma: no cover - environment dependent
+    import torch  # noqa: F401
+except ImportError:
+    pass
+
 lib = ctypes.CDLL(LIB_PATH)
 
 # status codes (tpl_status)
@@ -42,6 +52,8 @@ TPL_KERNEL_PASS1_SPMV = 0
 TPL_KERNEL_PASS1_AXPY = 1
 TPL_KERNEL_PASS2_SPMV = 2
 TPL_KERNEL_SPMV = 3
+TPL_KERNEL_PASS1_COMBINE = 4
+TPL_KERNEL_PASS2_COMBINE = 5
 
 PD = POINTER(c_double)
 
@@ -90,7 +102,7 @@ tpl_lanczos_pass_two = _sig("tpl_lanczos_pass_two", c_int, c_void_p, c_void_p, c
 tpl_load_kkt_system = _sig("tpl_load_kkt_system", c_int, c_char_p, c_char_p, POINTER(CsrHost))
 tpl_csr_host_free = _sig("tpl_csr_host_free", None, POINTER(CsrHost))
 tpl_op_schedule = _sig("tpl_op_schedule", c_int, c_void_p, POINTER(c_int32), POINTER(c_int32),
-                       POINTER(c_int32), POINTER(c_int32))
+                       POINTER(c_int32), POINTER(c_int64), POINTER(c_int32), POINTER(c_int32))
 tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_int32, c_int32,
                            c_int32)
 tpl_profile_kernel = _sig("tpl_profile_kernel", c_int, c_void_p, c_int, c_int, PD, PD)

@@ -109,17 +109,21 @@ class HipCsrOp:
 
     # -- schedule / measurement ------------------------------------------------
     def schedule(self):
-        """(items[n_items, 4] int32 {row0,row1,nz0,kind}, G, E) of the fused SpMV kernels."""
-        ni, g, e = c_int32(), c_int32(), c_int32()
-        check(_lib.tpl_op_schedule(self._op, byref(ni), byref(g), byref(e), None))
-        items = np.zeros((ni.value, 4), dtype=np.int32)
-        check(_lib.tpl_op_schedule(self._op, byref(ni), byref(g), byref(e),
-                                   items.ctypes.data_as(POINTER(c_int32))))
-        return items, g.value, e.value
+        """Device schedule: dict(items=[n_stream, 4] int32 {row0,row1,nz0,0},
+        long_rows=[n_long] int32, G2, E) — what the oracle needs to reproduce the
+        device reduction order."""
+        ns, nl, g2, e = c_int32(), c_int32(), c_int32(), c_int64()
+        check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e), None, None))
+        items = np.zeros((ns.value, 4), dtype=np.int32)
+        lr = np.zeros(max(nl.value, 1), dtype=np.int32)
+        check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e),
+                                   items.ctypes.data_as(POINTER(c_int32)),
+                                   lr.ctypes.data_as(POINTER(c_int32))))
+        return {"items": items, "long_rows": lr[:nl.value].copy(), "G2": g2.value, "E": e.value}
 
-    def set_schedule(self, stream_nnz_cap=0, stream_rows_cap=0, wave_row_max=0, max_groups=0):
-        check(_lib.tpl_op_set_schedule(self._op, stream_nnz_cap, stream_rows_cap, wave_row_max,
-                                       max_groups))
+    def set_schedule(self, stream_nnz_cap=0, stream_rows_cap=0, short_row_max=0, max_g2=0):
+        check(_lib.tpl_op_set_schedule(self._op, stream_nnz_cap, stream_rows_cap, short_row_max,
+                                       max_g2))
 
     def profile_kernel(self, kernel: int, iters: int = 200):
         """(avg microseconds per launch, algorithmic bytes per launch) via HIP events."""
