@@ -175,28 +175,25 @@ tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_c
 void tpl_csr_host_free(tpl_csr_host* csr);
 
 /* ---- introspection / measurement ---------------------------------------- */
-/* Schedule of the fused SpMV kernels (DESIGN.md "SpMV schedule"): rows with at most
- * short_row_max nnz are grouped into n_stream STREAM items {row0, row1, nz0, 0}
- * (one workgroup each); the n_long longer rows (ascending indices) are cut into 8
- * column slices processed by XCD-local workgroups and summed by a combine kernel.
+/* SpMV layout of the operator (DESIGN.md "SpMV layout"): rows with at most
+ * short_row_max nnz ("short", ascending) are stored as sliced ELL, 1024 rows per
+ * chunk, one workgroup each; the n_long longer rows (ascending) are cut into 8
+ * column slices handled by XCD-local workgroups and summed by the last arriver.
  * G2 workgroups of E elements run the element-wise kernels (= #norm partials).
- * items_out: 4 * n_stream int32 or NULL; long_rows_out: n_long int32 or NULL.
+ * short_rows_out: n_short int32 or NULL; long_rows_out: n_long int32 or NULL.
  * The CPU oracle uses this to reproduce the device reduction order bit for bit.   */
-tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_stream, int32_t* n_long, int32_t* G2,
-                           int64_t* E, int32_t* items_out, int32_t* long_rows_out);
-/* Schedule tuning (before the first solve; rebuilds the schedule; 0 = keep):
- * stream_nnz_cap <= 2048, stream_rows_cap <= 1024, short_row_max, max_g2.        */
-tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t stream_nnz_cap, int32_t stream_rows_cap,
-                               int32_t short_row_max, int32_t max_g2);
+tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_short, int32_t* n_long, int32_t* G2,
+                           int64_t* E, int32_t* short_rows_out, int32_t* long_rows_out);
+/* Layout tuning (rebuilds the layout; 0 = keep): short_row_max (default 32),
+ * max_g2 (default 1024).                                                         */
+tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g2);
 
 /* Kernel ids for tpl_profile_kernel */
 enum {
-  TPL_KERNEL_PASS1_SPMV = 0,    /* pass one: SpMV + beta-AXPY + alpha partials (short rows), long-row slices */
-  TPL_KERNEL_PASS1_AXPY = 1,    /* pass one: alpha-AXPY + ||w||^2 partials                                   */
-  TPL_KERNEL_PASS2_SPMV = 2,    /* pass two: SpMV + both AXPYs + scale + x += y v (short rows), slices       */
-  TPL_KERNEL_SPMV = 3,          /* plain y = A x (both kernels)                                              */
-  TPL_KERNEL_PASS1_COMBINE = 4, /* pass one: long rows from slice partials + epilogue                        */
-  TPL_KERNEL_PASS2_COMBINE = 5  /* pass two: long rows from slice partials + epilogue                        */
+  TPL_KERNEL_PASS1_SPMV = 0, /* pass one: SpMV + beta-AXPY + alpha partials             */
+  TPL_KERNEL_PASS1_AXPY = 1, /* pass one: alpha-AXPY + ||w||^2 partials                 */
+  TPL_KERNEL_PASS2_SPMV = 2, /* pass two: SpMV + both AXPYs + scale + x += y v          */
+  TPL_KERNEL_SPMV = 3        /* plain y = A x                                           */
 };
 /* Time `iters` back-to-back launches of one kernel on the operator's stream with
  * HIP events (a warm-up launch first). Returns the average per launch in

@@ -83,27 +83,16 @@ def md5_of_xz(path):
     return h.hexdigest()
 
 
-def canon_schedule(a, short_row_max=32, nnz_cap=2048, rows_cap=1024, max_g2=1024):
-    """The device's schedule rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp,
-    build_schedule) restated, for oracle runs without a GPU. The GPU tests take the
-    schedule from the live operator instead (HipCsrOp.schedule())."""
+def canon_schedule(a, short_row_max=32, max_g2=1024):
+    """The device's layout rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp, build_layout)
+    restated, for oracle runs without a GPU. The GPU tests take the layout from the
+    live operator instead (HipCsrOp.schedule())."""
     rp = a.indptr
     n = a.shape[0]
-    items, lrows = [], []
-    i = 0
-    while i < n:
-        if rp[i + 1] - rp[i] > short_row_max:
-            lrows.append(i)
-            i += 1
-            continue
-        r0, nz0, rows = i, rp[i], 0
-        while (i < n and rp[i + 1] - rp[i] <= short_row_max and rp[i + 1] - nz0 <= nnz_cap
-               and rows < rows_cap):
-            i += 1
-            rows += 1
-        items.append([r0, i, nz0, 0])
+    lens = np.diff(rp)
+    short = np.nonzero(lens <= short_row_max)[0].astype(np.int32)
+    long_ = np.nonzero(lens > short_row_max)[0].astype(np.int32)
     g2 = max(1, min(max_g2, -(-n // 1024)))
     per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)
-    return {"items": np.array(items, dtype=np.int32).reshape(-1, 4),
-            "long_rows": np.array(lrows, dtype=np.int32), "G2": g2, "E": E}
+    return {"short_rows": short, "long_rows": long_, "G2": g2, "E": E}

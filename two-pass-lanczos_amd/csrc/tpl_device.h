@@ -2,16 +2,22 @@
 // host runtime (tpl_runtime.cpp). Everything here is plain data: the kernels take
 // these structs by value as kernel arguments.
 //
-// SpMV schedule (built once per operator, tpl_runtime.cpp build_schedule):
-//   * short rows (<= kShortRowMax nnz) are grouped into STREAM items of consecutive
-//     rows (<= kStreamNnzCap nnz, <= kStreamRowsCap rows): one workgroup each, a
-//     coalesced sweep of the item's nnz into LDS, then one thread per row.
-//   * long rows are cut into kSlices column slices [s*n/8, (s+1)*n/8); a SLICE unit =
-//     (group of 4 long rows, slice s), one wave per row. Workgroup b of the SpMV grid
-//     handles slice b % 8: under the observed round-robin dispatch that keeps each
-//     XCD's L2 on 1/8 of the gathered vector (speed only, never correctness). Slice
-//     partials P[r][s] are summed by a small combine kernel, which also runs the
-//     long rows' epilogue.
+// SpMV layout (built once per operator, tpl_runtime.cpp build_layout):
+//   * SHORT rows (<= kShortRowMax nnz), taken in ascending order, are stored as
+//     sliced ELL: chunk c holds short-row positions [1024c, 1024c+1024); entry k of
+//     position p sits at chunk_base[c] + k*1024 + (p - 1024c) (column-major inside
+//     the chunk, padded to the chunk's widest row with col = -1). One workgroup per
+//     chunk, thread t owns positions 1024c + t + 256q: every CSR load is coalesced
+//     and no row pointer is chased. When every chunk has the same width and the
+//     short rows are exactly rows 0..n_short-1 (the KKT arc block), chunk bases and
+//     row indices are computed, not loaded.
+//   * LONG rows are cut into kSlices column slices [n*s/8, n*(s+1)/8); a SLICE unit =
+//     (group g of 4 long rows, slice s), one wave per row, handled by workgroup
+//     8g + s of the SpMV grid — under the observed round-robin dispatch each XCD's
+//     L2 then only caches 1/8 of the gathered vector (speed only, never
+//     correctness). Each unit publishes its 4 partials write-through (sc1) and bumps
+//     the group's counter; the 8th arriver sums the partials and runs the long rows'
+//     epilogue (split-K "last arriver" hand-off, cdna_hip_programming.md G16).
 //
 // Canonical reduction order (reproduced bit for bit by oracle/lanczos_oracle.c):
 //   * tree256(a[256])  : per 64-lane wave an xor butterfly (offsets 32,16,8,4,2,1,
@@ -20,10 +26,10 @@
 //   * short row        : s = 0; s += round(a_k x_k), k ascending.
 //   * long row         : per slice s: lane l: p_l = 0; p_l += round(a_k x_k) for
 //                        k = off[s] + l + 64q; P[s] = butterfly64(p); y = 0; y += P[s], s = 0..7.
-//   * alpha partial    : STREAM item i -> Pa[i]: thread t accumulates acc = fma(v, w, acc)
-//                        over its rows row0 + t + 256q, then tree256.
-//                        combine workgroup c -> Pa[n_stream + c]: thread t owns long row
-//                        256c + t (acc = fma(v, w, 0)), tree256.
+//   * alpha partial    : SHORT chunk c -> Pa[c]: thread t: acc = fma(v, w, acc) over its
+//                        positions 1024c + t + 256q (q = 0..3), tree256;
+//                        long group g -> Pa[n_chunks + g]: thread 64w holds
+//                        fma(v, w, 0) of long row 4g + w, all others 0, tree256.
 //   * norm partial     : workgroup b (of G2) owns [bE, min(n,(b+1)E)); thread t visits
 //                        i0 = bE + 2t + 512q, then i0, i0+1: acc = fma(x,x,acc); tree256.
 #pragma once
@@ -32,36 +38,41 @@
 namespace tpl {
 
 constexpr int kTPB = 256;            // threads per workgroup (4 waves of 64)
-constexpr int kStreamNnzCap = 2048;  // max nnz of one STREAM item (LDS product buffer)
-constexpr int kStreamRowsCap = 1024; // max rows of one STREAM item (4 rows per thread)
+constexpr int kChunkRows = 1024;     // short-row positions per SELL chunk (4 per thread)
+constexpr int kRowsPerThread = kChunkRows / kTPB;
 constexpr int kShortRowMax = 32;     // rows with more nnz are "long" (sliced)
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
 constexpr int kLongRowsPerGroup = 4; // one wave per row
 constexpr double kBreakdownTol = 2.220446049250313080847263336181640625e-13; // 1000*f64::EPSILON, src/algorithms/mod.rs:140-143
 
-struct Item {
-  int32_t row0, row1; // rows [row0, row1)
-  int32_t nz0;        // row_ptr[row0]
-  int32_t pad;
-};
-
-// Device view of the CSR operator plus its schedule.
+// Device view of the operator plus its layout.
 struct CsrDev {
-  const int32_t* row_ptr;  // n+1 (int32: nnz < 2^31)
-  const int32_t* col;      // nnz
-  const double* val;       // nnz
-  const Item* items;       // n_stream STREAM items
-  const int32_t* lrows;    // n_long long-row indices (ascending)
-  const int32_t* loff;     // n_long x (kSlices+1) slice offsets into col/val
-  double* P;               // n_long x kSlices slice partials
-  int32_t n_stream;
+  // long rows: CSR (global arrays, only long rows' entries are read)
+  const int32_t* row_ptr;   // n+1 (int32: nnz < 2^31)
+  const int32_t* col;       // nnz
+  const double* val;        // nnz
+  const int32_t* lrows;     // n_long long-row indices (ascending)
+  const int32_t* loff;      // n_long x (kSlices+1) slice offsets into col/val
+  double* P;                // n_long x kSlices slice partials (sc1 hand-off)
+  int32_t* cnt;             // n_groups arrival counters (zero between launches)
+  // short rows: sliced ELL
+  const int32_t* srows;     // n_short short-row indices (ascending); unused if s_identity
+  const int32_t* s_col;     // padded entries (col = -1 for padding)
+  const double* s_val;
+  const int32_t* c_base;    // n_chunks chunk base offsets; unused if s_width > 0
+  const int32_t* c_width;   // n_chunks chunk widths; unused if s_width > 0
+  int32_t s_width;          // > 0: every chunk has this width (bases computed)
+  int32_t s_identity;       // 1: short rows are exactly 0 .. n_short-1
+  int32_t n_short;
+  int32_t n_chunks;
   int32_t n_long;
-  int32_t n_slice_blocks;  // kSlices * ceil(n_long / 4); SpMV grid = n_slice_blocks + n_stream
-  int32_t n_comb_blocks;   // ceil(n_long / 256)
-  int32_t G2;              // workgroups of the element-wise kernels == #norm partials
-  int32_t NA;              // #alpha partials = n_stream + n_comb_blocks
+  int32_t n_groups;         // ceil(n_long / 4)
+  int32_t n_slice_blocks;   // kSlices * n_groups; SpMV grid = n_slice_blocks + n_chunks
+  int32_t G2;               // workgroups of the element-wise kernels == #norm partials
+  int32_t NA;               // #alpha partials = n_chunks + n_groups
+  int32_t pad;
   int64_t n;
-  int64_t E;               // elements per workgroup of the element-wise kernels
+  int64_t E;                // elements per workgroup of the element-wise kernels
 };
 
 // Device-resident solver state (one per operator).

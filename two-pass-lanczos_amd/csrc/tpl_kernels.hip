@@ -4,17 +4,15 @@
 //     w = A v_j ; w -= beta_{j-1} v_{j-1} ; alpha_j = v_j . w ; w -= alpha_j v_j ;
 //     beta_j = ||w|| ; v_{j+1} = w * (1/beta_j)
 // has two grid-wide dependencies (alpha before the second AXPY, beta before the
-// next SpMV). Pass one therefore runs per step:
-//   k_p1_spmv     [reduce beta partials -> beta_{j-1}, breakdown test]
-//                 fused SpMV gathering x = r_j * (1/beta_{j-1}) (the normalisation
-//                 v_j = w/beta folded into the gather, bit-identical to storing v_j);
-//                 short rows: full epilogue w = y - beta_{j-1} v_{j-1}, alpha partials;
-//                 long rows: column-slice partials only
-//   k_p1_combine  long rows: y = sum of slice partials, same epilogue, alpha partials
-//   k_p1_axpy     [reduce alpha partials -> alpha_j] r_{j+1} = w - alpha_j v_j ;
-//                 ||r_{j+1}||^2 partials
-// Pass two (src/algorithms/lanczos_two_pass.rs:176-312) knows every coefficient:
-//   k_p2_spmv + k_p2_combine: SpMV + both AXPYs + scale + x += y v.
+// next SpMV). Pass one therefore runs two launches per step:
+//   k_p1_spmv  [reduce beta partials -> beta_{j-1}, breakdown test]
+//              fused SpMV gathering x = r_j * (1/beta_{j-1}) (the normalisation
+//              v_j = w/beta folded into the gather, bit-identical to storing v_j);
+//              epilogue w = y - beta_{j-1} v_{j-1}; alpha partials
+//   k_p1_axpy  [reduce alpha partials -> alpha_j] r_{j+1} = w - alpha_j v_j ;
+//              ||r_{j+1}||^2 partials
+// Pass two (src/algorithms/lanczos_two_pass.rs:176-312) knows every coefficient, so
+// each step is ONE launch (k_p2_spmv): SpMV + both AXPYs + scale + x += y v.
 //
 // Arithmetic follows the reference op by op (-ffp-contract=off for this file):
 //   sub(w, mul(beta, v)) -> w - beta*v (two roundings), v = w * (1/beta)
@@ -23,17 +21,15 @@
 //   regenerates pass one's basis bit for bit (reference: basis_drift_fro = 0.0,
 //   results/orthogonality_*.csv).
 //
-// Memory-latency structure: every workgroup issues its independent global loads
-// (CSR arrays, row pointers, epilogue vectors, gathers) before it waits on the
-// grid-reduction prologue, so the partial-sum reduction overlaps the HBM/MALL
-// round trips instead of adding to them.
+// Latency structure (measured: a graph-launched empty kernel costs 1.6 us and each
+// dependent round of random gathers ~1.9 us on MI355X): every workgroup issues its
+// independent loads (stop flag, grid partials, CSR entries, epilogue vectors)
+// before its first wait, so a short-row chunk costs two memory round trips
+// (entries -> gathers) and the grid-reduction prologue hides under them.
 #include <hip/hip_runtime.h>
 #include "tpl_device.h"
 
 namespace tpl {
-
-constexpr int kNnzPerThread = kStreamNnzCap / kTPB; // 8
-constexpr int kRowsPerThread = kStreamRowsCap / kTPB; // 4
 
 // ---------------------------------------------------------------- reductions
 __device__ __forceinline__ double wave_sum(double v) {
@@ -81,8 +77,8 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
 }
 
 // ----------------------------------------------------------- epilogues
-// Each epilogue: pre(i) loads the row's own vector entries (issued early),
-// apply(i, s, pre, acc) finishes the row given its SpMV sum s.
+// pre(i) loads the row's own vector entries (issued early); apply(i, s, pre, acc)
+// finishes the row given its SpMV sum s (acc: the thread's alpha accumulator).
 struct PreNone {};
 struct EpiSpmv {
   double* y;
@@ -137,77 +133,129 @@ struct EpiPass2 {
   }
 };
 
-// --------------------------------------------------------------- SpMV pieces
-// A STREAM item: rows [row0,row1) with <= 2048 nnz. `scale_of()` is evaluated after
-// every independent load of the item is in flight (it may reduce grid partials).
+// Result of a workgroup's prologue: the gather scale, or "stop" (uniform across the grid).
+struct Scale {
+  double s;
+  bool ok;
+};
+struct UnitScale {
+  __device__ __forceinline__ Scale operator()() const { return Scale{1.0, true}; }
+};
+
+// ------------------------------------------------------ short rows (sliced ELL)
+constexpr int kFastWidth = 4; // widths up to this are fully unrolled
+
+// Gather phase of a short chunk: entries + x gathers in registers (fast path) ...
+struct ShortRegs {
+  int c[kRowsPerThread][kFastWidth];
+  double a[kRowsPerThread][kFastWidth];
+  double x[kRowsPerThread][kFastWidth];
+};
+
 template <class Epi, class ScaleFn>
-__device__ __forceinline__ void stream_item(const CsrDev& A, const Item item,
+__device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
                                             const double* __restrict__ xsrc, ScaleFn scale_of,
-                                            const Epi& epi, double* prod, double& acc,
-                                            double& scale_out) {
+                                            const Epi& epi, double& acc) {
   const int t = threadIdx.x;
-  const int nz0 = item.nz0;
-  // row pointers + epilogue inputs of this thread's rows (independent loads)
-  int rb[kRowsPerThread], re[kRowsPerThread];
-  decltype(epi.pre(0)) pr[kRowsPerThread];
+  int W, base;
+  if (A.s_width > 0) {
+    W = A.s_width;
+    base = chunk * kChunkRows * W;
+  } else {
+    W = A.c_width[chunk];
+    base = A.c_base[chunk];
+  }
+  int row[kRowsPerThread];
+  bool live[kRowsPerThread];
+  decltype(epi.pre(0)) pre[kRowsPerThread];
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) {
-    const int i = item.row0 + t + q * kTPB;
-    if (i < item.row1) {
-      rb[q] = A.row_ptr[i];
-      re[q] = A.row_ptr[i + 1];
-      pr[q] = epi.pre(i);
+    const int p = chunk * kChunkRows + q * kTPB + t;
+    live[q] = p < A.n_short;
+    row[q] = live[q] ? (A.s_identity ? p : A.srows[p]) : 0;
+  }
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q)
+    if (live[q]) pre[q] = epi.pre(row[q]);
+  const int off = t; // position inside the chunk: q * 256 + t
+  double s[kRowsPerThread];
+  if (W <= kFastWidth) {
+    ShortRegs R;
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q)
+#pragma unroll
+      for (int k = 0; k < kFastWidth; ++k) {
+        R.c[q][k] = -1;
+        if (live[q] && k < W) {
+          const int e = base + k * kChunkRows + q * kTPB + off;
+          R.c[q][k] = A.s_col[e];
+          R.a[q][k] = A.s_val[e];
+        }
+      }
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q)
+#pragma unroll
+      for (int k = 0; k < kFastWidth; ++k)
+        if (R.c[q][k] >= 0) R.x[q][k] = xsrc[R.c[q][k]];
+    const Scale sc = scale_of();
+    if (!sc.ok) return false; // stopped / breakdown (uniform)
+    const double scale = sc.s;
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q) {
+      double sum = 0.0;
+#pragma unroll
+      for (int k = 0; k < kFastWidth; ++k)
+        if (R.c[q][k] >= 0) sum = sum + R.a[q][k] * (R.x[q][k] * scale);
+      s[q] = sum;
+    }
+  } else {
+    const Scale sc = scale_of();
+    if (!sc.ok) return false;
+    const double scale = sc.s;
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q) s[q] = 0.0;
+    for (int k = 0; k < W; ++k) {
+      int c[kRowsPerThread];
+      double a[kRowsPerThread];
+#pragma unroll
+      for (int q = 0; q < kRowsPerThread; ++q) {
+        c[q] = -1;
+        if (live[q]) {
+          const int e = base + k * kChunkRows + q * kTPB + off;
+          c[q] = A.s_col[e];
+          a[q] = A.s_val[e];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kRowsPerThread; ++q)
+        if (c[q] >= 0) s[q] = s[q] + a[q] * (xsrc[c[q]] * scale);
     }
   }
-  const int cnt = A.row_ptr[item.row1] - nz0;
-  // coalesced sweep of the item's nnz + gathers
-  int cc[kNnzPerThread];
-  double aa[kNnzPerThread], xv[kNnzPerThread];
 #pragma unroll
-  for (int u = 0; u < kNnzPerThread; ++u) {
-    const int q = t + u * kTPB;
-    if (q < cnt) {
-      cc[u] = A.col[nz0 + q];
-      aa[u] = A.val[nz0 + q];
-    }
-  }
-#pragma unroll
-  for (int u = 0; u < kNnzPerThread; ++u) {
-    const int q = t + u * kTPB;
-    if (q < cnt) xv[u] = xsrc[cc[u]];
-  }
-  const double scale = scale_of(); // may wait on the grid-partials reduction
-  scale_out = scale;
-#pragma unroll
-  for (int u = 0; u < kNnzPerThread; ++u) {
-    const int q = t + u * kTPB;
-    if (q < cnt) prod[q] = aa[u] * (xv[u] * scale);
-  }
-  __syncthreads();
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    const int i = item.row0 + t + q * kTPB;
-    if (i < item.row1) {
-      double s = 0.0;
-      for (int k = rb[q] - nz0; k < re[q] - nz0; ++k) s = s + prod[k];
-      epi.apply(i, s, pr[q], acc);
-    }
-  }
+  for (int q = 0; q < kRowsPerThread; ++q)
+    if (live[q]) epi.apply(row[q], s[q], pre[q], acc);
+  return true;
 }
 
-// A SLICE unit: long rows 4g..4g+3 (one per wave), columns of slice s. Writes P[r][s].
-template <class ScaleFn>
-__device__ __forceinline__ void slice_unit(const CsrDev& A, int g, int s,
-                                           const double* __restrict__ xsrc, ScaleFn scale_of) {
+// -------------------------------------------------------- long rows (slices)
+// Slice unit (group g = 4 long rows, slice s). Returns true in the workgroup that
+// finalised the group (the 8th arriver); that workgroup's thread 64w has applied the
+// epilogue of long row 4g+w (acc updated).
+template <class Epi, class ScaleFn>
+__device__ __forceinline__ int slice_unit(const CsrDev& A, int g, int s,
+                                          const double* __restrict__ xsrc, ScaleFn scale_of,
+                                          const Epi& epi, double& acc, int* lds_flag) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ri = g * kLongRowsPerGroup + w;
   const bool live = ri < A.n_long;
-  int b = 0, e = 0;
+  int b = 0, e = 0, row = 0;
   if (live) {
     b = A.loff[ri * (kSlices + 1) + s];
     e = A.loff[ri * (kSlices + 1) + s + 1];
+    row = A.lrows[ri];
   }
-  // first batch of 4 entries per lane issued before the scale is known
+  decltype(epi.pre(0)) pre;
+  if (live && lane == 0) pre = epi.pre(row); // only the finalising workgroup uses it
   int q = b + lane;
   int c[4];
   double a[4], xv[4];
@@ -221,11 +269,13 @@ __device__ __forceinline__ void slice_unit(const CsrDev& A, int g, int s,
 #pragma unroll
   for (int u = 0; u < 4; ++u)
     if (q + 64 * u < e) xv[u] = xsrc[c[u]];
-  const double scale = scale_of();
-  double acc = 0.0;
+  const Scale sc = scale_of();
+  if (!sc.ok) return -1; // stopped / breakdown (uniform): counters untouched
+  const double scale = sc.s;
+  double p = 0.0;
 #pragma unroll
   for (int u = 0; u < 4; ++u)
-    if (q + 64 * u < e) acc = acc + a[u] * (xv[u] * scale);
+    if (q + 64 * u < e) p = p + a[u] * (xv[u] * scale);
   for (q += 256; q < e; q += 256) {
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -239,41 +289,59 @@ __device__ __forceinline__ void slice_unit(const CsrDev& A, int g, int s,
       if (q + 64 * u < e) xv[u] = xsrc[c[u]];
 #pragma unroll
     for (int u = 0; u < 4; ++u)
-      if (q + 64 * u < e) acc = acc + a[u] * (xv[u] * scale);
+      if (q + 64 * u < e) p = p + a[u] * (xv[u] * scale);
   }
-  acc = wave_sum(acc);
-  if (live && lane == 0) A.P[ri * kSlices + s] = acc;
+  p = wave_sum(p);
+  // Publish write-through (sc1), drain, count arrivals (split-K last-arriver form).
+  if (live && lane == 0)
+    __hip_atomic_store(&A.P[ri * kSlices + s], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const int old = __hip_atomic_fetch_add(&A.cnt[g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *lds_flag = (old == kSlices - 1);
+  }
+  __syncthreads();
+  const int last = *lds_flag;
+  if (last) {
+    if (threadIdx.x == 0)
+      __hip_atomic_store(&A.cnt[g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // next launch
+    if (live && lane == 0) {
+      double ps[kSlices];
+#pragma unroll
+      for (int k = 0; k < kSlices; ++k)
+        ps[k] = __hip_atomic_load(&A.P[ri * kSlices + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      double y = 0.0;
+#pragma unroll
+      for (int k = 0; k < kSlices; ++k) y = y + ps[k];
+      epi.apply(row, y, pre, acc);
+    }
+  }
+  return last;
 }
 
-// Long-row sum from its slice partials (canonical: y = 0; y += P[s], s ascending).
-__device__ __forceinline__ double combine_row(const CsrDev& A, int ri) {
-  double p[kSlices];
-#pragma unroll
-  for (int s = 0; s < kSlices; ++s) p[s] = A.P[ri * kSlices + s];
-  double y = 0.0;
-#pragma unroll
-  for (int s = 0; s < kSlices; ++s) y = y + p[s];
-  return y;
+// Workgroup dispatch of every SpMV-shaped kernel: [slice units][short chunks].
+// Returns the alpha-partial slot this workgroup owns (or -1: nothing to publish).
+template <class Epi, class ScaleFn>
+__device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
+                                          ScaleFn scale_of, const Epi& epi, double& acc,
+                                          int* lds_flag) {
+  const int b = blockIdx.x;
+  if (b < A.n_slice_blocks) {
+    const int g = b / kSlices;
+    const int last = slice_unit(A, g, b % kSlices, xsrc, scale_of, epi, acc, lds_flag);
+    return last == 1 ? A.n_chunks + g : -1;
+  }
+  const int chunk = b - A.n_slice_blocks;
+  return short_chunk(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
 }
 
 // ------------------------------------------------------------------ kernels
-// Grid of every SpMV kernel: [n_slice_blocks slice units][n_stream stream items].
 __global__ __launch_bounds__(kTPB) void k_spmv(CsrDev A, const double* __restrict__ x,
                                                double* __restrict__ y) {
-  __shared__ double prod[kStreamNnzCap];
-  const int b = blockIdx.x;
-  auto one = [] { return 1.0; };
-  if (b < A.n_slice_blocks) {
-    slice_unit(A, b / kSlices, b % kSlices, x, one);
-  } else {
-    double acc = 0.0, sc;
-    stream_item(A, A.items[b - A.n_slice_blocks], x, one, EpiSpmv{y}, prod, acc, sc);
-  }
-}
-
-__global__ __launch_bounds__(kTPB) void k_spmv_combine(CsrDev A, double* __restrict__ y) {
-  const int ri = blockIdx.x * kTPB + threadIdx.x;
-  if (ri < A.n_long) y[A.lrows[ri]] = combine_row(A, ri);
+  __shared__ int lds_flag;
+  double acc = 0.0;
+  spmv_block(A, x, UnitScale{}, EpiSpmv{y}, acc, &lds_flag);
 }
 
 // Pass-one prologue: ||b||^2 partials, reset flags.
@@ -302,105 +370,53 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
   if (threadIdx.x == 0) S.Pb[blockIdx.x] = p;
 }
 
-// beta_{j-1} from the norm partials; block 0 publishes it. Returns false on breakdown.
-__device__ __forceinline__ bool p1_beta(const CsrDev& A, const DevState& S, const PartialRegs& pr,
-                                        double* red, int j, double& beta) {
-  beta = sqrt(finish_partials(S.Pb, A.G2, pr, red)); // beta_{j-1} (||b|| at j = 1)
-  if (beta <= kBreakdownTol) {
-    // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
-    // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed (src/algorithms/lanczos_two_pass.rs:245-249).
-    if (blockIdx.x == 0 && threadIdx.x == 0) {
-      S.flags[0] = 1;
-      if (j == 1) S.flags[1] = 1;
-    }
-    return false;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    S.norms[j - 1] = beta;
-    if (j >= 2) S.betas[j - 2] = beta;
-  }
-  return true;
-}
-
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1).
 __global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ r_cur,
                                                   const double* __restrict__ r_prev,
                                                   double* __restrict__ W,
                                                   double* __restrict__ Vcol, int j) {
-  __shared__ double prod[kStreamNnzCap];
   __shared__ double red[4];
-  if (S.flags[0]) return; // stopped (breakdown / zero b) in an earlier launch
+  __shared__ int lds_flag;
+  const int stop = S.flags[0]; // checked after the loads are in flight
   PartialRegs pr;
   load_partials(S.Pb, A.G2, pr);
-  const int b = blockIdx.x;
-  bool ok = true;
-  if (b < A.n_slice_blocks) {
-    slice_unit(A, b / kSlices, b % kSlices, r_cur, [&] {
-      double beta;
-      ok = p1_beta(A, S, pr, red, j, beta);
-      return ok ? 1.0 / beta : 0.0;
-    });
-    return;
-  }
+  const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
   EpiPass1 epi;
   epi.r_cur = r_cur;
   epi.r_prev = (j >= 2) ? r_prev : nullptr;
-  epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
+  epi.invN_prev = (j >= 2) ? 1.0 / norm_prev : 0.0;
+  epi.invN_cur = 0.0;
+  epi.beta_sub = 0.0;
   epi.W = W;
   epi.Vcol = Vcol;
-  double beta = 0.0;
-  auto scale_fn = [&] {
-    ok = p1_beta(A, S, pr, red, j, beta);
-    return ok ? 1.0 / beta : 0.0;
-  };
-  // The epilogue's scale/beta are only known after scale_fn(); stream_item applies the
-  // epilogue after it, so fill them through a small indirection.
-  struct EpiLate {
-    EpiPass1* e;
-    const double* beta;
-    __device__ __forceinline__ Pre1 pre(int i) const { return e->pre(i); }
-    __device__ __forceinline__ void apply(int i, double s, const Pre1& p, double& acc) const {
-      EpiPass1 f = *e;
-      f.invN_cur = 1.0 / *beta;
-      f.beta_sub = f.r_prev ? *beta : 0.0;
-      f.apply(i, s, p, acc);
+  // beta_{j-1} (||b|| at j = 1) from the norm partials; fills the epilogue.
+  auto scale_fn = [&]() -> Scale {
+    if (stop) return Scale{0.0, false};
+    const double beta = sqrt(finish_partials(S.Pb, A.G2, pr, red));
+    if (beta <= kBreakdownTol) {
+      // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
+      // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed
+      //         (src/algorithms/lanczos_two_pass.rs:245-249).
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        S.flags[0] = 1;
+        if (j == 1) S.flags[1] = 1;
+      }
+      return Scale{0.0, false};
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+      S.norms[j - 1] = beta;
+      if (j >= 2) S.betas[j - 2] = beta;
+    }
+    epi.invN_cur = 1.0 / beta;
+    epi.beta_sub = (j >= 2) ? beta : 0.0;
+    return Scale{epi.invN_cur, true};
   };
-  double acc = 0.0, sc;
-  stream_item(A, A.items[b - A.n_slice_blocks], r_cur, scale_fn, EpiLate{&epi, &beta}, prod, acc,
-              sc);
-  if (!ok) return; // uniform: every thread of every workgroup computed the same beta
-  const double p = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pa[b - A.n_slice_blocks] = p;
-}
-
-// Pass one / standard: long rows from their slice partials, same epilogue.
-__global__ __launch_bounds__(kTPB) void k_p1_combine(CsrDev A, DevState S,
-                                                     const double* __restrict__ r_cur,
-                                                     const double* __restrict__ r_prev,
-                                                     double* __restrict__ W,
-                                                     double* __restrict__ Vcol, int j) {
-  __shared__ double red[4];
-  if (S.flags[0]) return;
-  const int ri = blockIdx.x * kTPB + threadIdx.x;
-  EpiPass1 epi;
-  epi.r_cur = r_cur;
-  epi.r_prev = (j >= 2) ? r_prev : nullptr;
-  const double beta = S.norms[j - 1];
-  epi.invN_cur = 1.0 / beta;
-  epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
-  epi.beta_sub = (j >= 2) ? beta : 0.0;
-  epi.W = W;
-  epi.Vcol = Vcol;
   double acc = 0.0;
-  if (ri < A.n_long) {
-    const int r = A.lrows[ri];
-    const Pre1 p = epi.pre(r);
-    epi.apply(r, combine_row(A, ri), p, acc);
-  }
-  const double part = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pa[A.n_stream + blockIdx.x] = part;
+  const int slot = spmv_block(A, r_cur, scale_fn, epi, acc, &lds_flag);
+  if (slot < 0) return; // uniform per workgroup
+  const double p = block_sum(acc, red);
+  if (threadIdx.x == 0) S.Pa[slot] = p;
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
@@ -409,25 +425,27 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   const double* __restrict__ r_cur,
                                                   double* __restrict__ r_next, int j, int k) {
   __shared__ double red[4];
-  if (S.flags[0]) return;
+  const int stop = S.flags[0];
   PartialRegs pr;
   load_partials(S.Pa, A.NA, pr);
   const int64_t beg = (int64_t)blockIdx.x * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
-  const double invN = 1.0 / S.norms[j - 1];
-  // first pair of this thread issued before alpha is known
+  const double normj = S.norms[j - 1];
+  // this thread's first pair issued before alpha is known
   const int64_t i00 = beg + 2 * threadIdx.x;
   double2 w0 = make_double2(0.0, 0.0), rc0 = make_double2(0.0, 0.0);
   if (j < k && i00 + 1 < end) {
     w0 = *reinterpret_cast<const double2*>(W + i00);
     rc0 = *reinterpret_cast<const double2*>(r_cur + i00);
   }
+  if (stop) return;
   const double alpha = finish_partials(S.Pa, A.NA, pr, red);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
   }
   if (j == k) return; // beta_k is never used (src/algorithms/lanczos_two_pass.rs:252-254)
+  const double invN = 1.0 / normj;
   double acc = 0.0;
   for (int64_t i0 = i00; i0 < end; i0 += 2 * kTPB) {
     if (i0 + 1 < end) {
@@ -472,9 +490,14 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
   }
 }
 
-__device__ __forceinline__ EpiPass2 p2_epi(const DevState& S, const double* v_cur,
-                                           const double* v_prev, double* v_next, double* x,
-                                           double* Vcol, int j) {
+// Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x.
+__global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
+                                                  const double* __restrict__ v_cur,
+                                                  const double* __restrict__ v_prev,
+                                                  double* __restrict__ v_next,
+                                                  double* __restrict__ x,
+                                                  double* __restrict__ Vcol, int j) {
+  __shared__ int lds_flag;
   EpiPass2 epi;
   epi.v_cur = v_cur;
   epi.v_prev = (j >= 2) ? v_prev : nullptr;
@@ -485,42 +508,8 @@ __device__ __forceinline__ EpiPass2 p2_epi(const DevState& S, const double* v_cu
   epi.v_next = v_next;
   epi.x = x;
   epi.Vcol = Vcol;
-  return epi;
-}
-
-// Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x (short rows; long
-// rows' slice partials).
-__global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
-                                                  const double* __restrict__ v_cur,
-                                                  const double* __restrict__ v_prev,
-                                                  double* __restrict__ v_next,
-                                                  double* __restrict__ x,
-                                                  double* __restrict__ Vcol, int j) {
-  __shared__ double prod[kStreamNnzCap];
-  const int b = blockIdx.x;
-  auto one = [] { return 1.0; };
-  if (b < A.n_slice_blocks) {
-    slice_unit(A, b / kSlices, b % kSlices, v_cur, one);
-    return;
-  }
-  const EpiPass2 epi = p2_epi(S, v_cur, v_prev, v_next, x, Vcol, j);
-  double acc = 0.0, sc;
-  stream_item(A, A.items[b - A.n_slice_blocks], v_cur, one, epi, prod, acc, sc);
-}
-
-__global__ __launch_bounds__(kTPB) void k_p2_combine(CsrDev A, DevState S,
-                                                     const double* __restrict__ v_cur,
-                                                     const double* __restrict__ v_prev,
-                                                     double* __restrict__ v_next,
-                                                     double* __restrict__ x,
-                                                     double* __restrict__ Vcol, int j) {
-  const int ri = blockIdx.x * kTPB + threadIdx.x;
-  if (ri >= A.n_long) return;
-  const EpiPass2 epi = p2_epi(S, v_cur, v_prev, v_next, x, Vcol, j);
-  const int r = A.lrows[ri];
-  const Pre2 p = epi.pre(r);
   double acc = 0.0;
-  epi.apply(r, combine_row(A, ri), p, acc);
+  spmv_block(A, v_cur, UnitScale{}, epi, acc, &lds_flag);
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
@@ -622,12 +611,10 @@ static inline int elem_grid(int64_t n) {
   if (g < 1) g = 1;
   return (int)g;
 }
-static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + A.n_stream; }
+static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + A.n_chunks; }
 
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s) {
   if (spmv_grid(A) > 0) hipLaunchKernelGGL(k_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, x, y);
-  if (A.n_comb_blocks > 0)
-    hipLaunchKernelGGL(k_spmv_combine, dim3(A.n_comb_blocks), dim3(kTPB), 0, s, A, y);
   return hipGetLastError();
 }
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s) {
@@ -639,21 +626,6 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, cons
   if (spmv_grid(A) > 0)
     hipLaunchKernelGGL(k_p1_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, r_cur, r_prev, W,
                        Vcol, j);
-  if (A.n_comb_blocks > 0)
-    hipLaunchKernelGGL(k_p1_combine, dim3(A.n_comb_blocks), dim3(kTPB), 0, s, A, S, r_cur, r_prev,
-                       W, Vcol, j);
-  return hipGetLastError();
-}
-hipError_t p1_spmv_only(const CsrDev& A, const DevState& S, const double* r_cur,
-                        const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, r_cur, r_prev, W,
-                     Vcol, j);
-  return hipGetLastError();
-}
-hipError_t p1_combine_only(const CsrDev& A, const DevState& S, const double* r_cur,
-                           const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_combine, dim3(A.n_comb_blocks > 0 ? A.n_comb_blocks : 1), dim3(kTPB), 0,
-                     s, A, S, r_cur, r_prev, W, Vcol, j);
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
@@ -671,23 +643,6 @@ hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, cons
   if (spmv_grid(A) > 0)
     hipLaunchKernelGGL(k_p2_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, v_cur, v_prev,
                        v_next, x, Vcol, j);
-  if (A.n_comb_blocks > 0)
-    hipLaunchKernelGGL(k_p2_combine, dim3(A.n_comb_blocks), dim3(kTPB), 0, s, A, S, v_cur, v_prev,
-                       v_next, x, Vcol, j);
-  return hipGetLastError();
-}
-hipError_t p2_spmv_only(const CsrDev& A, const DevState& S, const double* v_cur,
-                        const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                        hipStream_t s) {
-  hipLaunchKernelGGL(k_p2_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, v_cur, v_prev, v_next,
-                     x, Vcol, j);
-  return hipGetLastError();
-}
-hipError_t p2_combine_only(const CsrDev& A, const DevState& S, const double* v_cur,
-                           const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                           hipStream_t s) {
-  hipLaunchKernelGGL(k_p2_combine, dim3(A.n_comb_blocks > 0 ? A.n_comb_blocks : 1), dim3(kTPB), 0,
-                     s, A, S, v_cur, v_prev, v_next, x, Vcol, j);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,

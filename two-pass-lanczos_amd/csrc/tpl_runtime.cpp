@@ -30,18 +30,8 @@ hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s);
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
                    double* W, double* Vcol, int j, hipStream_t s);
-hipError_t p1_spmv_only(const CsrDev& A, const DevState& S, const double* r_cur,
-                        const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
-hipError_t p1_combine_only(const CsrDev& A, const DevState& S, const double* r_cur,
-                           const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s);
-hipError_t p2_spmv_only(const CsrDev& A, const DevState& S, const double* v_cur,
-                        const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                        hipStream_t s);
-hipError_t p2_combine_only(const CsrDev& A, const DevState& S, const double* v_cur,
-                           const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                           hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, hipStream_t s);
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
@@ -101,59 +91,87 @@ static tpl_status guarded(F&& f) {
   }
 }
 
-// ------------------------------------------------------------ schedule
+// ------------------------------------------------------------ layout
 struct SchedParams {
-  int stream_nnz_cap = kStreamNnzCap;
-  int stream_rows_cap = kStreamRowsCap;
   int short_row_max = kShortRowMax; // rows longer than this are sliced
   int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
 };
 
-struct Schedule {
-  std::vector<Item> items;      // STREAM items
-  std::vector<int32_t> lrows;   // long rows, ascending
-  std::vector<int32_t> loff;    // n_long x (kSlices + 1)
+// Host copy of the SpMV layout (tpl_device.h).
+struct Layout {
+  std::vector<int32_t> srows;       // short rows, ascending
+  std::vector<int32_t> s_col;       // sliced ELL entries (col = -1: padding)
+  std::vector<double> s_val;
+  std::vector<int32_t> c_base, c_width;
+  int32_t s_width = 0;              // uniform chunk width (0: per-chunk)
+  int32_t s_identity = 0;
+  std::vector<int32_t> lrows;       // long rows, ascending
+  std::vector<int32_t> loff;        // n_long x (kSlices + 1)
   int G2 = 1;
   int64_t E = 512;
 };
 
-// Short rows -> STREAM items of consecutive short rows; long rows -> sliced units.
-static Schedule build_schedule(int64_t n, const std::vector<int32_t>& rp,
-                               const std::vector<int32_t>& col, const SchedParams& sp) {
-  Schedule S;
-  auto len = [&](int64_t r) { return (int64_t)rp[r + 1] - rp[r]; };
-  int64_t i = 0;
-  while (i < n) {
-    if (len(i) > sp.short_row_max) {
-      S.lrows.push_back((int32_t)i);
-      ++i;
-      continue;
+static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
+                           const std::vector<int32_t>& col, const std::vector<double>& val,
+                           const SchedParams& sp) {
+  Layout L;
+  for (int64_t i = 0; i < n; ++i) {
+    if (rp[i + 1] - rp[i] > sp.short_row_max) L.lrows.push_back((int32_t)i);
+    else L.srows.push_back((int32_t)i);
+  }
+  const int64_t ns = (int64_t)L.srows.size();
+  L.s_identity = 1;
+  for (int64_t p = 0; p < ns; ++p)
+    if (L.srows[p] != p) {
+      L.s_identity = 0;
+      break;
     }
-    const int64_t row0 = i, nz0 = rp[i];
-    int rows = 0;
-    while (i < n && len(i) <= sp.short_row_max && (int64_t)rp[i + 1] - nz0 <= sp.stream_nnz_cap &&
-           rows < sp.stream_rows_cap) {
-      ++i;
-      ++rows;
+  const int64_t nchunks = (ns + kChunkRows - 1) / kChunkRows;
+  L.c_base.resize(nchunks);
+  L.c_width.resize(nchunks);
+  int64_t total = 0;
+  for (int64_t c = 0; c < nchunks; ++c) {
+    int32_t w = 0;
+    for (int64_t p = c * kChunkRows; p < std::min(ns, (c + 1) * kChunkRows); ++p)
+      w = std::max<int32_t>(w, rp[L.srows[p] + 1] - rp[L.srows[p]]);
+    L.c_base[c] = (int32_t)total;
+    L.c_width[c] = w;
+    total += (int64_t)w * kChunkRows;
+  }
+  if (total >= INT32_MAX) fail(TPL_ERR_UNSUPPORTED, "sliced-ELL storage exceeds 2^31 entries");
+  L.s_col.assign(std::max<int64_t>(total, 1), -1);
+  L.s_val.assign(std::max<int64_t>(total, 1), 0.0);
+  for (int64_t c = 0; c < nchunks; ++c)
+    for (int64_t p = c * kChunkRows; p < std::min(ns, (c + 1) * kChunkRows); ++p) {
+      const int32_t r = L.srows[p];
+      for (int32_t k = 0; k < rp[r + 1] - rp[r]; ++k) {
+        const int64_t e = L.c_base[c] + (int64_t)k * kChunkRows + (p - c * kChunkRows);
+        L.s_col[e] = col[rp[r] + k];
+        L.s_val[e] = val[rp[r] + k];
+      }
     }
-    S.items.push_back(Item{(int32_t)row0, (int32_t)i, (int32_t)nz0, 0});
+  L.s_width = 0;
+  if (nchunks > 0) {
+    bool uni = true;
+    for (int64_t c = 0; c < nchunks; ++c) uni = uni && L.c_width[c] == L.c_width[0];
+    if (uni && L.c_width[0] > 0) L.s_width = L.c_width[0];
   }
   // slice offsets: first entry of long row r with column >= floor(n * s / kSlices)
-  S.loff.resize(S.lrows.size() * (kSlices + 1));
-  for (size_t r = 0; r < S.lrows.size(); ++r) {
-    const int32_t row = S.lrows[r];
+  L.loff.resize(L.lrows.size() * (kSlices + 1));
+  for (size_t r = 0; r < L.lrows.size(); ++r) {
+    const int32_t row = L.lrows[r];
     int32_t q = rp[row];
     for (int s = 0; s <= kSlices; ++s) {
       const int64_t bound = n * s / kSlices;
       while (q < rp[row + 1] && col[q] < bound) ++q;
-      S.loff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
+      L.loff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
     }
   }
   const int64_t g2 = (n + 1023) / 1024;
-  S.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
-  const int64_t per = (n + S.G2 - 1) / S.G2;
-  S.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
-  return S;
+  L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
+  const int64_t per = (n + L.G2 - 1) / L.G2;
+  L.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
+  return L;
 }
 
 } // namespace tpl
@@ -180,12 +198,18 @@ struct tpl_op_s {
   int32_t* d_col = nullptr;
   double* d_val = nullptr;
   std::vector<int32_t> h_col;
+  std::vector<double> h_val;
   SchedParams sp;
-  Schedule sched;
-  Item* d_items = nullptr;
+  Layout lay;
   int32_t* d_lrows = nullptr;
   int32_t* d_loff = nullptr;
   double* d_P = nullptr;
+  int32_t* d_cnt = nullptr;
+  int32_t* d_srows = nullptr;
+  int32_t* d_scol = nullptr;
+  double* d_sval = nullptr;
+  int32_t* d_cbase = nullptr;
+  int32_t* d_cwidth = nullptr;
   // vectors: b, R0..R2, W, x, V2_0..V2_2, tmp (n each, padded)
   double* d_vecs = nullptr;
   int64_t ld = 0;
@@ -211,22 +235,32 @@ bool use_graphs() {
 }
 
 CsrDev csr_dev(const tpl_op_s* op) {
+  const Layout& L = op->lay;
   CsrDev A;
   A.row_ptr = op->d_rowptr;
   A.col = op->d_col;
   A.val = op->d_val;
-  A.items = op->d_items;
   A.lrows = op->d_lrows;
   A.loff = op->d_loff;
   A.P = op->d_P;
-  A.n_stream = (int32_t)op->sched.items.size();
-  A.n_long = (int32_t)op->sched.lrows.size();
-  A.n_slice_blocks = kSlices * ((A.n_long + kLongRowsPerGroup - 1) / kLongRowsPerGroup);
-  A.n_comb_blocks = (A.n_long + kTPB - 1) / kTPB;
-  A.G2 = op->sched.G2;
-  A.NA = A.n_stream + A.n_comb_blocks;
+  A.cnt = op->d_cnt;
+  A.srows = op->d_srows;
+  A.s_col = op->d_scol;
+  A.s_val = op->d_sval;
+  A.c_base = op->d_cbase;
+  A.c_width = op->d_cwidth;
+  A.s_width = L.s_width;
+  A.s_identity = L.s_identity;
+  A.n_short = (int32_t)L.srows.size();
+  A.n_chunks = (int32_t)L.c_base.size();
+  A.n_long = (int32_t)L.lrows.size();
+  A.n_groups = (A.n_long + kLongRowsPerGroup - 1) / kLongRowsPerGroup;
+  A.n_slice_blocks = kSlices * A.n_groups;
+  A.G2 = L.G2;
+  A.NA = A.n_chunks + A.n_groups;
+  A.pad = 0;
   A.n = op->n;
-  A.E = op->sched.E;
+  A.E = L.E;
   return A;
 }
 
@@ -245,16 +279,27 @@ void upload(T** dst, const std::vector<T>& src) {
 }
 
 void rebuild_schedule(tpl_op_s* op) {
-  op->sched = build_schedule(op->n, op->h_rowptr, op->h_col, op->sp);
-  upload(&op->d_items, op->sched.items);
-  upload(&op->d_lrows, op->sched.lrows);
-  upload(&op->d_loff, op->sched.loff);
+  op->lay = build_layout(op->n, op->h_rowptr, op->h_col, op->h_val, op->sp);
+  const Layout& L = op->lay;
+  upload(&op->d_lrows, L.lrows);
+  upload(&op->d_loff, L.loff);
+  upload(&op->d_srows, L.srows);
+  upload(&op->d_scol, L.s_col);
+  upload(&op->d_sval, L.s_val);
+  upload(&op->d_cbase, L.c_base);
+  upload(&op->d_cwidth, L.c_width);
   if (op->d_P) HIPCHK(hipFree(op->d_P));
+  if (op->d_cnt) HIPCHK(hipFree(op->d_cnt));
   op->d_P = nullptr;
-  if (!op->sched.lrows.empty())
-    HIPCHK(hipMalloc(&op->d_P, op->sched.lrows.size() * kSlices * sizeof(double)));
+  op->d_cnt = nullptr;
+  if (!L.lrows.empty()) {
+    const size_t groups = (L.lrows.size() + kLongRowsPerGroup - 1) / kLongRowsPerGroup;
+    HIPCHK(hipMalloc(&op->d_P, L.lrows.size() * kSlices * sizeof(double)));
+    HIPCHK(hipMalloc(&op->d_cnt, groups * sizeof(int32_t)));
+    HIPCHK(hipMemset(op->d_cnt, 0, groups * sizeof(int32_t))); // arrival counters start at 0
+  }
   drop_graphs(op);
-  // partial buffers depend on the schedule: force state reallocation
+  // partial buffers depend on the layout: force state reallocation
   op->kcap = 0;
 }
 
@@ -287,7 +332,7 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
   }
   if (reorth && !op->d_Pr) {
     // [cols x G partials][cols coefficients]
-    HIPCHK(hipMalloc(&op->d_Pr, ((size_t)op->sched.G2 + 1) * op->kcap * sizeof(double)));
+    HIPCHK(hipMalloc(&op->d_Pr, ((size_t)op->lay.G2 + 1) * op->kcap * sizeof(double)));
   }
 }
 
@@ -329,8 +374,8 @@ inline const double* r_of(const tpl_op_s* op, int j) { return j == 1 ? op->b : o
 // applied twice, of r_{j+1} against the stored columns V[:, 0..j) before beta_j.
 void enqueue_reorth(tpl_op_s* op, int j) {
   const int cols = j; // v_1 .. v_j are stored in V[:, 0..j)
-  const int G2 = op->sched.G2;
-  const int64_t E = op->sched.E;
+  const int G2 = op->lay.G2;
+  const int64_t E = op->lay.E;
   double* P = op->d_Pr;                             // cols x G2 partials
   double* h = op->d_Pr + (size_t)G2 * op->kcap;    // cols coefficients
   double* r = op->R[(j + 1) % 3];
@@ -538,6 +583,7 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
     op->h_rowptr.resize(n + 1);
     for (int64_t i = 0; i <= n; ++i) op->h_rowptr[i] = (int32_t)row_ptr[i];
     op->h_col.assign(col_idx, col_idx + nnz);
+    op->h_val.assign(vals, vals + nnz);
     HIPCHK(hipMalloc(&op->d_rowptr, (n + 1) * sizeof(int32_t)));
     HIPCHK(hipMemcpy(op->d_rowptr, op->h_rowptr.data(), (n + 1) * sizeof(int32_t),
                      hipMemcpyHostToDevice));
@@ -577,10 +623,10 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipFree(op->d_rowptr);
     hipFree(op->d_col);
     hipFree(op->d_val);
-    if (op->d_items) hipFree(op->d_items);
-    if (op->d_lrows) hipFree(op->d_lrows);
-    if (op->d_loff) hipFree(op->d_loff);
-    if (op->d_P) hipFree(op->d_P);
+    for (void* p : {(void*)op->d_lrows, (void*)op->d_loff, (void*)op->d_P, (void*)op->d_cnt,
+                    (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval, (void*)op->d_cbase,
+                    (void*)op->d_cwidth})
+      if (p) hipFree(p);
     hipFree(op->d_vecs);
     if (op->d_state) hipFree(op->d_state);
     if (op->h_state) hipHostFree(op->h_state);
@@ -772,41 +818,25 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
   });
 }
 
-tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_stream, int32_t* n_long, int32_t* G2,
-                           int64_t* E, int32_t* items_out, int32_t* long_rows_out) {
+tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_short, int32_t* n_long, int32_t* G2,
+                           int64_t* E, int32_t* short_rows_out, int32_t* long_rows_out) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
-    const Schedule& S = op->sched;
-    if (n_stream) *n_stream = (int32_t)S.items.size();
-    if (n_long) *n_long = (int32_t)S.lrows.size();
-    if (G2) *G2 = S.G2;
-    if (E) *E = S.E;
-    if (items_out)
-      for (size_t i = 0; i < S.items.size(); ++i) {
-        items_out[4 * i + 0] = S.items[i].row0;
-        items_out[4 * i + 1] = S.items[i].row1;
-        items_out[4 * i + 2] = S.items[i].nz0;
-        items_out[4 * i + 3] = 0;
-      }
-    if (long_rows_out)
-      for (size_t i = 0; i < S.lrows.size(); ++i) long_rows_out[i] = S.lrows[i];
+    const Layout& L = op->lay;
+    if (n_short) *n_short = (int32_t)L.srows.size();
+    if (n_long) *n_long = (int32_t)L.lrows.size();
+    if (G2) *G2 = L.G2;
+    if (E) *E = L.E;
+    if (short_rows_out) std::copy(L.srows.begin(), L.srows.end(), short_rows_out);
+    if (long_rows_out) std::copy(L.lrows.begin(), L.lrows.end(), long_rows_out);
   });
 }
 
-tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t stream_nnz_cap, int32_t stream_rows_cap,
-                               int32_t short_row_max, int32_t max_g2) {
+tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g2) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     set_device(op);
-    if (stream_nnz_cap > 0) {
-      if (stream_nnz_cap > kStreamNnzCap) fail(TPL_ERR_INVALID_ARGUMENT, "stream_nnz_cap > 2048");
-      op->sp.stream_nnz_cap = stream_nnz_cap;
-    }
-    if (stream_rows_cap > 0) {
-      if (stream_rows_cap > kStreamRowsCap) fail(TPL_ERR_INVALID_ARGUMENT, "stream_rows_cap > 1024");
-      op->sp.stream_rows_cap = stream_rows_cap;
-    }
-    if (short_row_max > 0) op->sp.short_row_max = std::min(short_row_max, op->sp.stream_nnz_cap);
+    if (short_row_max > 0) op->sp.short_row_max = short_row_max;
     if (max_g2 > 0) op->sp.max_g2 = max_g2;
     HIPCHK(hipStreamSynchronize(op->stream));
     rebuild_schedule(op);
@@ -822,20 +852,17 @@ tpl_status tpl_copy_to_host(void* dst, const void* src_device, size_t bytes) {
 }
 
 double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
+  // B_spmv = 12 nnz + 4 (n+1) + 16 n (fp64 value + int32 column per
+  // nonzero, int32 row_ptr, x read once, y written once). The fused kernels add the
+  // epilogue vectors they must touch (DESIGN.md "Algorithmic bytes").
   if (!op) return 0.0;
   const double n = (double)op->n, nnz = (double)op->nnz;
-  const double nl = (double)op->sched.lrows.size(), ns = n - nl;
-  // CSR: fp64 value + int32 column per nnz, int32 row_ptr; the gathered vector
-  // counted once (8n), slice metadata 36 B and 8 partials per long row.
-  const double csr = 12.0 * nnz + 4.0 * (n + 1.0);
-  const double slices = nl * (4.0 * (kSlices + 1) + 8.0 * kSlices);
+  const double spmv = 12.0 * nnz + 4.0 * (n + 1.0) + 16.0 * n;
   switch (kernel) {
-    case TPL_KERNEL_SPMV: return csr + 8.0 * n + 8.0 * ns + slices;            // x; y (short rows)
-    case TPL_KERNEL_PASS1_SPMV: return csr + 8.0 * n + 16.0 * ns + slices;     // r_j; r_{j-1}, w (short rows)
-    case TPL_KERNEL_PASS1_COMBINE: return nl * (8.0 * kSlices + 4.0 + 24.0);   // partials; r_j, r_{j-1}, w
-    case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;                               // w, r_j read; r_{j+1} written
-    case TPL_KERNEL_PASS2_SPMV: return csr + 8.0 * n + 32.0 * ns + slices;     // v_j; v_{j-1}, x, v_{j+1}, x (short rows)
-    case TPL_KERNEL_PASS2_COMBINE: return nl * (8.0 * kSlices + 4.0 + 40.0);
+    case TPL_KERNEL_SPMV: return spmv;
+    case TPL_KERNEL_PASS1_SPMV: return spmv + 8.0 * n;   // + r_{j-1} read (w is the y write)
+    case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;         // w, r_j read; r_{j+1} written
+    case TPL_KERNEL_PASS2_SPMV: return spmv + 24.0 * n;  // + v_{j-1}, x read, x written
     default: return 0.0;
   }
 }
@@ -852,21 +879,14 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
       switch (kernel) {
         case TPL_KERNEL_SPMV: HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream)); break;
         case TPL_KERNEL_PASS1_SPMV:
-          HIPCHK(launch::p1_spmv_only(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
-          break;
-        case TPL_KERNEL_PASS1_COMBINE:
-          HIPCHK(launch::p1_combine_only(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
+          HIPCHK(launch::p1_spmv(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
           break;
         case TPL_KERNEL_PASS1_AXPY:
           HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
-          HIPCHK(launch::p2_spmv_only(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr, 2,
-                                      op->stream));
-          break;
-        case TPL_KERNEL_PASS2_COMBINE:
-          HIPCHK(launch::p2_combine_only(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr,
-                                         2, op->stream));
+          HIPCHK(launch::p2_spmv(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr, 2,
+                                 op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }

@@ -52,8 +52,6 @@ TPL_KERNEL_PASS1_SPMV = 0
 TPL_KERNEL_PASS1_AXPY = 1
 TPL_KERNEL_PASS2_SPMV = 2
 TPL_KERNEL_SPMV = 3
-TPL_KERNEL_PASS1_COMBINE = 4
-TPL_KERNEL_PASS2_COMBINE = 5
 
 PD = POINTER(c_double)
 
@@ -103,8 +101,7 @@ tpl_load_kkt_system = _sig("tpl_load_kkt_system", c_int, c_char_p, c_char_p, POI
 tpl_csr_host_free = _sig("tpl_csr_host_free", None, POINTER(CsrHost))
 tpl_op_schedule = _sig("tpl_op_schedule", c_int, c_void_p, POINTER(c_int32), POINTER(c_int32),
                        POINTER(c_int32), POINTER(c_int64), POINTER(c_int32), POINTER(c_int32))
-tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_int32, c_int32,
-                           c_int32)
+tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_int32)
 tpl_profile_kernel = _sig("tpl_profile_kernel", c_int, c_void_p, c_int, c_int, PD, PD)
 tpl_kernel_algo_bytes = _sig("tpl_kernel_algo_bytes", c_double, c_void_p, c_int)
 tpl_copy_to_host = _sig("tpl_copy_to_host", c_int, c_void_p, c_void_p, c_size_t)

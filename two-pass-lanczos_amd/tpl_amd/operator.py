@@ -109,21 +109,20 @@ class HipCsrOp:
 
     # -- schedule / measurement ------------------------------------------------
     def schedule(self):
-        """Device schedule: dict(items=[n_stream, 4] int32 {row0,row1,nz0,0},
-        long_rows=[n_long] int32, G2, E) — what the oracle needs to reproduce the
-        device reduction order."""
+        """Device layout: dict(short_rows, long_rows, G2, E) — what the oracle needs to
+        reproduce the device reduction order."""
         ns, nl, g2, e = c_int32(), c_int32(), c_int32(), c_int64()
         check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e), None, None))
-        items = np.zeros((ns.value, 4), dtype=np.int32)
+        sr = np.zeros(max(ns.value, 1), dtype=np.int32)
         lr = np.zeros(max(nl.value, 1), dtype=np.int32)
         check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e),
-                                   items.ctypes.data_as(POINTER(c_int32)),
+                                   sr.ctypes.data_as(POINTER(c_int32)),
                                    lr.ctypes.data_as(POINTER(c_int32))))
-        return {"items": items, "long_rows": lr[:nl.value].copy(), "G2": g2.value, "E": e.value}
+        return {"short_rows": sr[:ns.value].copy(), "long_rows": lr[:nl.value].copy(),
+                "G2": g2.value, "E": e.value}
 
-    def set_schedule(self, stream_nnz_cap=0, stream_rows_cap=0, short_row_max=0, max_g2=0):
-        check(_lib.tpl_op_set_schedule(self._op, stream_nnz_cap, stream_rows_cap, short_row_max,
-                                       max_g2))
+    def set_schedule(self, short_row_max=0, max_g2=0):
+        check(_lib.tpl_op_set_schedule(self._op, short_row_max, max_g2))
 
     def profile_kernel(self, kernel: int, iters: int = 200):
         """(avg microseconds per launch, algorithmic bytes per launch) via HIP events."""
