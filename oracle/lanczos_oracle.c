@@ -52,8 +52,8 @@ typedef struct {
   int64_t E;             /* elements per element-wise workgroup */
 } osched;
 
-#define CHUNK 1024       /* short-row positions per sliced-ELL chunk */
-#define GROUP 4          /* long rows per slice unit */
+#define CHUNK 256        /* short-row positions per sliced-ELL chunk */
+#define GROUP 16         /* long rows per slice unit (4 per wave) */
 
 #define SLICES 8
 
@@ -129,9 +129,9 @@ static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
 
 /* ------------------------------------------------------------ dot / norm */
 /* alpha = v . w in device order: short chunk c -> partial c (thread t owns short
- * positions 1024c + t + 256q, q = 0..3, fma accumulation, tree256); long group g ->
- * partial n_chunks + g (thread 64w holds fma(v, w, 0) of long row 4g + w);
- * then reduce_partials. */
+ * positions CHUNK*c + t + 256q, fma accumulation, tree256); long group g ->
+ * partial n_chunks + g (thread 64w accumulates fma over long rows 16g + w + 4i,
+ * i = 0..3); then reduce_partials. */
 static double dot_canon(const osched* S, const double* v, const double* w, double* P) {
   double acc[TPB];
   const int32_t nch = (S->n_short + CHUNK - 1) / CHUNK;
@@ -148,10 +148,11 @@ static double dot_canon(const osched* S, const double* v, const double* w, doubl
   const int32_t ng = (S->n_long + GROUP - 1) / GROUP;
   for (int32_t g = 0; g < ng; ++g) {
     for (int t = 0; t < TPB; ++t) acc[t] = 0.0;
-    for (int wv = 0; wv < GROUP; ++wv) {
-      const int32_t ri = g * GROUP + wv;
-      if (ri < S->n_long) acc[64 * wv] = fma(v[S->lrows[ri]], w[S->lrows[ri]], 0.0);
-    }
+    for (int wv = 0; wv < 4; ++wv)
+      for (int i = 0; i < GROUP / 4; ++i) {
+        const int32_t ri = g * GROUP + wv + 4 * i;
+        if (ri < S->n_long) acc[64 * wv] = fma(v[S->lrows[ri]], w[S->lrows[ri]], acc[64 * wv]);
+      }
     P[nch + g] = tree256(acc);
   }
   return reduce_partials(P, nch + ng);

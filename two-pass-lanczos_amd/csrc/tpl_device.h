@@ -4,18 +4,18 @@
 //
 // SpMV layout (built once per operator, tpl_runtime.cpp build_layout):
 //   * SHORT rows (<= kShortRowMax nnz), taken in ascending order, are stored as
-//     sliced ELL: chunk c holds short-row positions [1024c, 1024c+1024); entry k of
-//     position p sits at chunk_base[c] + k*1024 + (p - 1024c) (column-major inside
-//     the chunk, padded to the chunk's widest row with col = -1). One workgroup per
-//     chunk, thread t owns positions 1024c + t + 256q: every CSR load is coalesced
+//     sliced ELL: chunk c holds short-row positions [C*c, C*c + C) (C = kChunkRows);
+//     entry k of position p sits at chunk_base[c] + k*C + (p - C*c) (column-major
+//     inside the chunk, padded to the chunk's widest row with col = -1). One workgroup
+//     per chunk, thread t owns positions C*c + t + 256q: every CSR load is coalesced
 //     and no row pointer is chased. When every chunk has the same width and the
 //     short rows are exactly rows 0..n_short-1 (the KKT arc block), chunk bases and
 //     row indices are computed, not loaded.
 //   * LONG rows are cut into kSlices column slices [n*s/8, n*(s+1)/8); a SLICE unit =
-//     (group g of 4 long rows, slice s), one wave per row, handled by workgroup
-//     8g + s of the SpMV grid — under the observed round-robin dispatch each XCD's
-//     L2 then only caches 1/8 of the gathered vector (speed only, never
-//     correctness). Each unit publishes its 4 partials write-through (sc1) and bumps
+//     (group g of 16 long rows, slice s): wave w walks rows 16g + w + 4i (i = 0..3),
+//     handled by workgroup n_chunks + 8g + s of the SpMV grid (chunks first) — under
+//     the observed round-robin dispatch each XCD's L2 then only caches 1/8 of the
+//     gathered vector (speed only, never correctness). Each unit publishes its 4 partials write-through (sc1) and bumps
 //     the group's counter; the 8th arriver sums the partials and runs the long rows'
 //     epilogue (split-K "last arriver" hand-off, cdna_hip_programming.md G16).
 //
@@ -27,9 +27,9 @@
 //   * long row         : per slice s: lane l: p_l = 0; p_l += round(a_k x_k) for
 //                        k = off[s] + l + 64q; P[s] = butterfly64(p); y = 0; y += P[s], s = 0..7.
 //   * alpha partial    : SHORT chunk c -> Pa[c]: thread t: acc = fma(v, w, acc) over its
-//                        positions 1024c + t + 256q (q = 0..3), tree256;
-//                        long group g -> Pa[n_chunks + g]: thread 64w holds
-//                        fma(v, w, 0) of long row 4g + w, all others 0, tree256.
+//                        positions kChunkRows*c + t + 256q (q ascending), tree256;
+//                        long group g -> Pa[n_chunks + g]: thread 64w: acc = fma(v, w, acc)
+//                        over long rows 16g + w + 4i (i = 0..3), all others 0, tree256.
 //   * norm partial     : workgroup b (of G2) owns [bE, min(n,(b+1)E)); thread t visits
 //                        i0 = bE + 2t + 512q, then i0, i0+1: acc = fma(x,x,acc); tree256.
 #pragma once
@@ -38,11 +38,18 @@
 namespace tpl {
 
 constexpr int kTPB = 256;            // threads per workgroup (4 waves of 64)
-constexpr int kChunkRows = 1024;     // short-row positions per SELL chunk (4 per thread)
+#ifndef TPL_CHUNK_ROWS
+#define TPL_CHUNK_ROWS 256
+#endif
+constexpr int kChunkRows = TPL_CHUNK_ROWS; // short-row positions per SELL chunk
 constexpr int kRowsPerThread = kChunkRows / kTPB;
 constexpr int kShortRowMax = 32;     // rows with more nnz are "long" (sliced)
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
-constexpr int kLongRowsPerGroup = 4; // one wave per row
+#ifndef TPL_LONG_ROWS_PER_WAVE
+#define TPL_LONG_ROWS_PER_WAVE 4
+#endif
+constexpr int kLongRowsPerWave = TPL_LONG_ROWS_PER_WAVE;  // long rows a wave walks in turn
+constexpr int kLongRowsPerGroup = 4 * kLongRowsPerWave;    // long rows per slice unit
 constexpr double kBreakdownTol = 2.220446049250313080847263336181640625e-13; // 1000*f64::EPSILON, src/algorithms/mod.rs:140-143
 
 // Device view of the operator plus its layout.
@@ -66,8 +73,8 @@ struct CsrDev {
   int32_t n_short;
   int32_t n_chunks;
   int32_t n_long;
-  int32_t n_groups;         // ceil(n_long / 4)
-  int32_t n_slice_blocks;   // kSlices * n_groups; SpMV grid = n_slice_blocks + n_chunks
+  int32_t n_groups;         // ceil(n_long / kLongRowsPerGroup)
+  int32_t n_slice_blocks;   // kSlices * n_groups; SpMV grid = n_chunks + n_slice_blocks
   int32_t G2;               // workgroups of the element-wise kernels == #norm partials
   int32_t NA;               // #alpha partials = n_chunks + n_groups
   int32_t pad;

@@ -29,6 +29,13 @@
 #include <hip/hip_runtime.h>
 #include "tpl_device.h"
 
+// Performance-ablation switches for experiments only (scripts/ablate.sh builds
+// separate libraries); production builds have TPL_ABLATE == 0. Bit 1: skip the
+// slice units; 2: skip the short chunks; 4: no last-arriver hand-off.
+#ifndef TPL_ABLATE
+#define TPL_ABLATE 0
+#endif
+
 namespace tpl {
 
 // ---------------------------------------------------------------- reductions
@@ -58,12 +65,13 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 struct PartialRegs {
   double v[8];
 };
+// (Every load below is unconditional with a clamped index and its result masked
+// afterwards: a load under a runtime condition makes hipcc branch around it and
+// drain vmcnt per element, serialising the round trips — guide §5 trap (c).)
+__device__ __forceinline__ int clampi(int i, int hi) { return i < hi ? i : hi; }
 __device__ __forceinline__ void load_partials(const double* __restrict__ P, int N, PartialRegs& r) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
-    const int i = threadIdx.x + u * kTPB;
-    r.v[u] = i < N ? P[i] : 0.0;
-  }
+  for (int u = 0; u < 8; ++u) r.v[u] = P[clampi(threadIdx.x + u * kTPB, N - 1)];
 }
 // ... and reduce them later in the canonical order (s = 0; s += P[t + 256q]).
 __device__ __forceinline__ double finish_partials(const double* __restrict__ P, int N,
@@ -92,16 +100,15 @@ struct Pre1 {
 };
 struct EpiPass1 {
   const double* r_cur;  // r_j (v_j = r_j * invN_cur)
-  const double* r_prev; // r_{j-1} or nullptr (j == 1: v_0 = 0)
+  const double* r_prev; // r_{j-1}; == r_cur (never used) at j == 1 where v_0 = 0
+  bool has_prev;
   double invN_cur, invN_prev, beta_sub;
   double* W;
   double* Vcol;         // standard variant: column j-1 of V_k, else nullptr
-  __device__ __forceinline__ Pre1 pre(int i) const {
-    return Pre1{r_cur[i], r_prev ? r_prev[i] : 0.0};
-  }
+  __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
   __device__ __forceinline__ void apply(int i, double s, const Pre1& p, double& acc) const {
     const double v = p.rc * invN_cur;
-    const double vp = r_prev ? p.rp * invN_prev : 0.0;
+    const double vp = has_prev ? p.rp * invN_prev : 0.0;
     const double w = s - beta_sub * vp;
     W[i] = w;
     if (Vcol) Vcol[i] = v;
@@ -115,16 +122,16 @@ struct Pre2 {
 };
 struct EpiPass2 {
   const double* v_cur;
-  const double* v_prev; // nullptr at j == 1
+  const double* v_prev; // == v_cur (never used) at j == 1 where v_0 = 0
+  bool has_prev;
   double beta_sub, alpha, invb, ycoef;
   double* v_next;
   double* x;
   double* Vcol; // lanczos_pass_two_with_basis: column j of V'_k, else nullptr
-  __device__ __forceinline__ Pre2 pre(int i) const {
-    return Pre2{v_cur[i], v_prev ? v_prev[i] : 0.0, x[i]};
-  }
+  __device__ __forceinline__ Pre2 pre(int i) const { return Pre2{v_cur[i], v_prev[i], x[i]}; }
   __device__ __forceinline__ void apply(int i, double s, const Pre2& p, double&) const {
-    double w = s - beta_sub * p.vp;
+    const double vp = has_prev ? p.vp : 0.0;
+    double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
     v_next[i] = vn;
@@ -143,28 +150,13 @@ struct UnitScale {
 };
 
 // ------------------------------------------------------ short rows (sliced ELL)
-constexpr int kFastWidth = 4; // widths up to this are fully unrolled
-
-// Gather phase of a short chunk: entries + x gathers in registers (fast path) ...
-struct ShortRegs {
-  int c[kRowsPerThread][kFastWidth];
-  double a[kRowsPerThread][kFastWidth];
-  double x[kRowsPerThread][kFastWidth];
-};
-
-template <class Epi, class ScaleFn>
-__device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
-                                            const double* __restrict__ xsrc, ScaleFn scale_of,
-                                            const Epi& epi, double& acc) {
+// Chunk with a compile-time width W (entries loaded unconditionally: the sliced-ELL
+// storage is allocated for whole chunks, padding has col = -1).
+template <int W, class Epi, class ScaleFn>
+__device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int base,
+                                              const double* __restrict__ xsrc, ScaleFn scale_of,
+                                              const Epi& epi, double& acc) {
   const int t = threadIdx.x;
-  int W, base;
-  if (A.s_width > 0) {
-    W = A.s_width;
-    base = chunk * kChunkRows * W;
-  } else {
-    W = A.c_width[chunk];
-    base = A.c_base[chunk];
-  }
   int row[kRowsPerThread];
   bool live[kRowsPerThread];
   decltype(epi.pre(0)) pre[kRowsPerThread];
@@ -172,63 +164,78 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
   for (int q = 0; q < kRowsPerThread; ++q) {
     const int p = chunk * kChunkRows + q * kTPB + t;
     live[q] = p < A.n_short;
-    row[q] = live[q] ? (A.s_identity ? p : A.srows[p]) : 0;
+    const int pc = clampi(p, A.n_short - 1);
+    row[q] = A.s_identity ? pc : A.srows[pc];
   }
 #pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
+  int c[kRowsPerThread][W];
+  double a[kRowsPerThread][W], xv[kRowsPerThread][W];
+#pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q)
-    if (live[q]) pre[q] = epi.pre(row[q]);
-  const int off = t; // position inside the chunk: q * 256 + t
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const int e = base + k * kChunkRows + q * kTPB + t;
+      c[q][k] = A.s_col[e];
+      a[q][k] = A.s_val[e];
+    }
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q)
+#pragma unroll
+    for (int k = 0; k < W; ++k) xv[q][k] = xsrc[c[q][k] < 0 ? 0 : c[q][k]];
+  const Scale sc = scale_of();
+  if (!sc.ok) return false; // stopped / breakdown (uniform)
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    double sum = 0.0;
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+      const double nxt = sum + a[q][k] * (xv[q][k] * sc.s);
+      sum = c[q][k] >= 0 ? nxt : sum;
+    }
+    if (live[q]) epi.apply(row[q], sum, pre[q], acc);
+  }
+  return true;
+}
+
+// Any width: entries in batches of 4 per row.
+template <class Epi, class ScaleFn>
+__device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int base, int W,
+                                                const double* __restrict__ xsrc, ScaleFn scale_of,
+                                                const Epi& epi, double& acc) {
+  const int t = threadIdx.x;
+  int row[kRowsPerThread];
+  bool live[kRowsPerThread];
+  decltype(epi.pre(0)) pre[kRowsPerThread];
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    const int p = chunk * kChunkRows + q * kTPB + t;
+    live[q] = p < A.n_short;
+    const int pc = clampi(p, A.n_short - 1);
+    row[q] = A.s_identity ? pc : A.srows[pc];
+  }
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
+  const Scale sc = scale_of();
+  if (!sc.ok) return false;
   double s[kRowsPerThread];
-  if (W <= kFastWidth) {
-    ShortRegs R;
 #pragma unroll
-    for (int q = 0; q < kRowsPerThread; ++q)
-#pragma unroll
-      for (int k = 0; k < kFastWidth; ++k) {
-        R.c[q][k] = -1;
-        if (live[q] && k < W) {
-          const int e = base + k * kChunkRows + q * kTPB + off;
-          R.c[q][k] = A.s_col[e];
-          R.a[q][k] = A.s_val[e];
-        }
-      }
-#pragma unroll
-    for (int q = 0; q < kRowsPerThread; ++q)
-#pragma unroll
-      for (int k = 0; k < kFastWidth; ++k)
-        if (R.c[q][k] >= 0) R.x[q][k] = xsrc[R.c[q][k]];
-    const Scale sc = scale_of();
-    if (!sc.ok) return false; // stopped / breakdown (uniform)
-    const double scale = sc.s;
+  for (int q = 0; q < kRowsPerThread; ++q) s[q] = 0.0;
+  for (int k = 0; k < W; ++k) {
+    int c[kRowsPerThread];
+    double a[kRowsPerThread], xv[kRowsPerThread];
 #pragma unroll
     for (int q = 0; q < kRowsPerThread; ++q) {
-      double sum = 0.0;
-#pragma unroll
-      for (int k = 0; k < kFastWidth; ++k)
-        if (R.c[q][k] >= 0) sum = sum + R.a[q][k] * (R.x[q][k] * scale);
-      s[q] = sum;
+      const int e = base + k * kChunkRows + q * kTPB + t;
+      c[q] = A.s_col[e];
+      a[q] = A.s_val[e];
     }
-  } else {
-    const Scale sc = scale_of();
-    if (!sc.ok) return false;
-    const double scale = sc.s;
 #pragma unroll
-    for (int q = 0; q < kRowsPerThread; ++q) s[q] = 0.0;
-    for (int k = 0; k < W; ++k) {
-      int c[kRowsPerThread];
-      double a[kRowsPerThread];
+    for (int q = 0; q < kRowsPerThread; ++q) xv[q] = xsrc[c[q] < 0 ? 0 : c[q]];
 #pragma unroll
-      for (int q = 0; q < kRowsPerThread; ++q) {
-        c[q] = -1;
-        if (live[q]) {
-          const int e = base + k * kChunkRows + q * kTPB + off;
-          c[q] = A.s_col[e];
-          a[q] = A.s_val[e];
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < kRowsPerThread; ++q)
-        if (c[q] >= 0) s[q] = s[q] + a[q] * (xsrc[c[q]] * scale);
+    for (int q = 0; q < kRowsPerThread; ++q) {
+      const double nxt = s[q] + a[q] * (xv[q] * sc.s);
+      s[q] = c[q] >= 0 ? nxt : s[q];
     }
   }
 #pragma unroll
@@ -237,64 +244,115 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
   return true;
 }
 
+template <class Epi, class ScaleFn>
+__device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
+                                            const double* __restrict__ xsrc, ScaleFn scale_of,
+                                            const Epi& epi, double& acc) {
+  int W, base;
+  if (A.s_width > 0) {
+    W = A.s_width;
+    base = chunk * kChunkRows * W;
+  } else {
+    W = A.c_width[chunk];
+    base = A.c_base[chunk];
+  }
+  switch (W) {
+    case 1: return short_chunk_w<1>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 2: return short_chunk_w<2>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 3: return short_chunk_w<3>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 4: return short_chunk_w<4>(A, chunk, base, xsrc, scale_of, epi, acc);
+    default: return short_chunk_any(A, chunk, base, W, xsrc, scale_of, epi, acc);
+  }
+}
+
 // -------------------------------------------------------- long rows (slices)
-// Slice unit (group g = 4 long rows, slice s). Returns true in the workgroup that
-// finalised the group (the 8th arriver); that workgroup's thread 64w has applied the
-// epilogue of long row 4g+w (acc updated).
+// Slice unit (group g of 16 long rows, slice s): wave w walks rows 16g + w + 4i.
+// Returns 1 in the workgroup that finalised the group (the 8th arriver; its thread
+// 64w applied the epilogue of its rows, acc updated), 0 otherwise, -1 if stopped.
 template <class Epi, class ScaleFn>
 __device__ __forceinline__ int slice_unit(const CsrDev& A, int g, int s,
                                           const double* __restrict__ xsrc, ScaleFn scale_of,
                                           const Epi& epi, double& acc, int* lds_flag) {
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ri = g * kLongRowsPerGroup + w;
-  const bool live = ri < A.n_long;
-  int b = 0, e = 0, row = 0;
-  if (live) {
-    b = A.loff[ri * (kSlices + 1) + s];
-    e = A.loff[ri * (kSlices + 1) + s + 1];
-    row = A.lrows[ri];
-  }
-  decltype(epi.pre(0)) pre;
-  if (live && lane == 0) pre = epi.pre(row); // only the finalising workgroup uses it
-  int q = b + lane;
-  int c[4];
-  double a[4], xv[4];
+  int ri[kLongRowsPerWave], row[kLongRowsPerWave], b[kLongRowsPerWave], e[kLongRowsPerWave];
+  bool live[kLongRowsPerWave];
+  decltype(epi.pre(0)) pre[kLongRowsPerWave];
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    if (q + 64 * u < e) {
-      c[u] = A.col[q + 64 * u];
-      a[u] = A.val[q + 64 * u];
+  for (int i = 0; i < kLongRowsPerWave; ++i) {
+    ri[i] = g * kLongRowsPerGroup + w + 4 * i;
+    live[i] = ri[i] < A.n_long;
+    const int ric = clampi(ri[i], A.n_long - 1);
+    b[i] = A.loff[ric * (kSlices + 1) + s];
+    e[i] = A.loff[ric * (kSlices + 1) + s + 1];
+    row[i] = A.lrows[ric];
+    if (!live[i]) e[i] = b[i];
+  }
+#pragma unroll
+  for (int i = 0; i < kLongRowsPerWave; ++i) pre[i] = epi.pre(row[i]); // finaliser only
+  // first batch: 2 entries per lane of every row, issued before the scale is known
+  int c0[kLongRowsPerWave][2];
+  double a0[kLongRowsPerWave][2], x0[kLongRowsPerWave][2];
+#pragma unroll
+  for (int i = 0; i < kLongRowsPerWave; ++i)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int k = clampi(b[i] + lane + 64 * u, e[i] > b[i] ? e[i] - 1 : b[i]);
+      c0[i][u] = A.col[k];
+      a0[i][u] = A.val[k];
     }
-  }
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (q + 64 * u < e) xv[u] = xsrc[c[u]];
+  for (int i = 0; i < kLongRowsPerWave; ++i)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) x0[i][u] = xsrc[c0[i][u]];
   const Scale sc = scale_of();
   if (!sc.ok) return -1; // stopped / breakdown (uniform): counters untouched
   const double scale = sc.s;
-  double p = 0.0;
+  double p[kLongRowsPerWave];
 #pragma unroll
-  for (int u = 0; u < 4; ++u)
-    if (q + 64 * u < e) p = p + a[u] * (xv[u] * scale);
-  for (q += 256; q < e; q += 256) {
+  for (int i = 0; i < kLongRowsPerWave; ++i) {
+    p[i] = 0.0;
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      if (q + 64 * u < e) {
-        c[u] = A.col[q + 64 * u];
-        a[u] = A.val[q + 64 * u];
+    for (int u = 0; u < 2; ++u) {
+      const double nxt = p[i] + a0[i][u] * (x0[i][u] * scale);
+      p[i] = (b[i] + lane + 64 * u < e[i]) ? nxt : p[i];
+    }
+  }
+  // remaining entries, 4 per lane per batch
+#pragma unroll
+  for (int i = 0; i < kLongRowsPerWave; ++i) {
+    const int last_e = e[i] > b[i] ? e[i] - 1 : b[i];
+    for (int q = b[i] + lane + 128; q < e[i]; q += 256) {
+      int c[4];
+      double a[4], xv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = clampi(q + 64 * u, last_e);
+        c[u] = A.col[k];
+        a[u] = A.val[k];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) xv[u] = xsrc[c[u]];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const double nxt = p[i] + a[u] * (xv[u] * scale);
+        p[i] = (q + 64 * u < e[i]) ? nxt : p[i];
       }
     }
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (q + 64 * u < e) xv[u] = xsrc[c[u]];
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if (q + 64 * u < e) p = p + a[u] * (xv[u] * scale);
   }
-  p = wave_sum(p);
+#pragma unroll
+  for (int i = 0; i < kLongRowsPerWave; ++i) p[i] = wave_sum(p[i]);
+  if (TPL_ABLATE & 4) {
+#pragma unroll
+    for (int i = 0; i < kLongRowsPerWave; ++i)
+      if (live[i] && lane == 0) A.P[ri[i] * kSlices + s] = p[i];
+    return 0;
+  }
   // Publish write-through (sc1), drain, count arrivals (split-K last-arriver form).
-  if (live && lane == 0)
-    __hip_atomic_store(&A.P[ri * kSlices + s], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+  for (int i = 0; i < kLongRowsPerWave; ++i)
+    if (live[i] && lane == 0)
+      __hip_atomic_store(&A.P[ri[i] * kSlices + s], p[i], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -306,33 +364,45 @@ __device__ __forceinline__ int slice_unit(const CsrDev& A, int g, int s,
   if (last) {
     if (threadIdx.x == 0)
       __hip_atomic_store(&A.cnt[g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // next launch
-    if (live && lane == 0) {
-      double ps[kSlices];
+    if (lane == 0) {
+      double ps[kLongRowsPerWave][kSlices];
 #pragma unroll
-      for (int k = 0; k < kSlices; ++k)
-        ps[k] = __hip_atomic_load(&A.P[ri * kSlices + k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      double y = 0.0;
+      for (int i = 0; i < kLongRowsPerWave; ++i)
 #pragma unroll
-      for (int k = 0; k < kSlices; ++k) y = y + ps[k];
-      epi.apply(row, y, pre, acc);
+        for (int k = 0; k < kSlices; ++k)
+          ps[i][k] = __hip_atomic_load(&A.P[clampi(ri[i], A.n_long - 1) * kSlices + k],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int i = 0; i < kLongRowsPerWave; ++i) {
+        double y = 0.0;
+#pragma unroll
+        for (int k = 0; k < kSlices; ++k) y = y + ps[i][k];
+        if (live[i]) epi.apply(row[i], y, pre[i], acc);
+      }
     }
   }
   return last;
 }
 
-// Workgroup dispatch of every SpMV-shaped kernel: [slice units][short chunks].
-// Returns the alpha-partial slot this workgroup owns (or -1: nothing to publish).
+#ifndef TPL_CHUNKS_FIRST
+#define TPL_CHUNKS_FIRST 1
+#endif
 template <class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
                                           ScaleFn scale_of, const Epi& epi, double& acc,
                                           int* lds_flag) {
-  const int b = blockIdx.x;
+  int b = blockIdx.x;
+  if (TPL_CHUNKS_FIRST) { // [chunks][slices]: slice s of group g at n_chunks + 8g + s
+    b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
+  }
   if (b < A.n_slice_blocks) {
+    if (TPL_ABLATE & 1) return -1;
     const int g = b / kSlices;
     const int last = slice_unit(A, g, b % kSlices, xsrc, scale_of, epi, acc, lds_flag);
     return last == 1 ? A.n_chunks + g : -1;
   }
   const int chunk = b - A.n_slice_blocks;
+  if (TPL_ABLATE & 2) return -1;
   return short_chunk(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
 }
 
@@ -384,7 +454,8 @@ __global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
   const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
   EpiPass1 epi;
   epi.r_cur = r_cur;
-  epi.r_prev = (j >= 2) ? r_prev : nullptr;
+  epi.r_prev = (j >= 2) ? r_prev : r_cur;
+  epi.has_prev = j >= 2;
   epi.invN_prev = (j >= 2) ? 1.0 / norm_prev : 0.0;
   epi.invN_cur = 0.0;
   epi.beta_sub = 0.0;
@@ -500,7 +571,8 @@ __global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
   __shared__ int lds_flag;
   EpiPass2 epi;
   epi.v_cur = v_cur;
-  epi.v_prev = (j >= 2) ? v_prev : nullptr;
+  epi.v_prev = (j >= 2) ? v_prev : v_cur;
+  epi.has_prev = j >= 2;
   epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
   epi.alpha = S.alphas[j - 1];
   epi.invb = 1.0 / S.betas[j - 1];

@@ -12,7 +12,8 @@ import os
 from ctypes import (CFUNCTYPE, POINTER, c_char, c_char_p, c_double, c_int, c_int32,
                     c_int64, c_size_t, c_void_p)
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libtpl_amd.so")
+LIB_PATH = os.environ.get("TPL_LIB_PATH") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "libtpl_amd.so")  # override: experiments only
 
 if not os.path.exists(LIB_PATH):
     raise ImportError(
