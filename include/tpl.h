@@ -184,9 +184,20 @@ void tpl_csr_host_free(tpl_csr_host* csr);
  * The CPU oracle uses this to reproduce the device reduction order bit for bit.   */
 tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_short, int32_t* n_long, int32_t* G2,
                            int64_t* E, int32_t* short_rows_out, int32_t* long_rows_out);
-/* Layout tuning (rebuilds the layout; 0 = keep): short_row_max (default 32),
- * max_g2 (default 1024).                                                         */
+/* Layout tuning (rebuilds the layout; 0 = keep): short_row_max (> 0: explicit,
+ * -1: the default auto rule T = clamp(2 * median row nnz, 4, 32)), max_g2
+ * (default 1024).                                                                */
 tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g2);
+
+/* Live timing of the solver's own launches: with timing on, HIP events on the
+ * operator's stream bracket pass one's graph and the graph of pass two's step
+ * launches (its prologue then runs as a separate launch), so the numbers come from
+ * the very launches of the last solve, inside the caller's timed region.
+ * pass2_spmv_us / pass2_launches is the average duration of one pass-two step
+ * launch (k_p2_spmv), launch gaps included.                                      */
+tpl_status tpl_op_enable_timing(tpl_op_t op, int on);
+tpl_status tpl_op_pass_timing(tpl_op_t op, double* pass1_us, double* pass2_spmv_us,
+                              int64_t* pass2_launches);
 
 /* Kernel ids for tpl_profile_kernel */
 enum {

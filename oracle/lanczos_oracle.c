@@ -52,15 +52,17 @@ typedef struct {
   int64_t E;             /* elements per element-wise workgroup */
 } osched;
 
-#define CHUNK 256        /* short-row positions per sliced-ELL chunk */
-#define GROUP 16         /* long rows per slice unit (4 per wave) */
+#define CHUNK 512        /* short-row positions per sliced-ELL chunk (kChunkRows) */
 
 #define SLICES 8
 
 /* ------------------------------------------------------------ trees */
-static double tree64(double* a) { /* xor butterfly == pairwise (l, l+half) tree */
-  for (int half = 32; half >= 1; half >>= 1)
-    for (int l = 0; l < half; ++l) a[l] = a[l] + a[l + half];
+static double tree64(double* a) { /* xor butterfly, offsets 1, 2, 4, 8, 16, 32 */
+  double nx[64];
+  for (int h = 1; h < 64; h <<= 1) {
+    for (int l = 0; l < 64; ++l) nx[l] = a[l] + a[l ^ h];
+    memcpy(a, nx, sizeof(nx));
+  }
   return a[0];
 }
 static double tree256(const double* a) {
@@ -89,8 +91,9 @@ static void spmv_faithful(const ocsr* A, const double* x, double* y) {
   }
 }
 
-/* long row: per slice s (columns [n*s/8, n*(s+1)/8)) lane l sums entries
- * off_s + l + 64q; butterfly64 -> P[s]; y = 0; y += P[s] (s ascending). */
+/* long row: per slice s (columns [floor(n*s/8), floor(n*(s+1)/8))) lane g (0..7)
+ * sums the slice's entries g + 8q; butterfly over the 8 lanes (xor 1, 2, 4) -> P_s;
+ * y = 0; y += P_s (s ascending). */
 static double long_row_canon(const ocsr* A, int32_t i, const double* x) {
   const int64_t n = A->n;
   int64_t q = A->rp[i];
@@ -99,14 +102,17 @@ static double long_row_canon(const ocsr* A, int32_t i, const double* x) {
     const int64_t bound = (s + 1 == SLICES) ? INT64_MAX : n * (s + 1) / SLICES;
     int64_t e = q;
     while (e < A->rp[i + 1] && A->ci[e] < bound) ++e;
-    if (s + 1 == SLICES) e = A->rp[i + 1];
-    double lane[64];
-    for (int l = 0; l < 64; ++l) {
+    double lane[8], nx[8];
+    for (int g = 0; g < 8; ++g) {
       double p = 0.0;
-      for (int64_t k = q + l; k < e; k += 64) p = p + A->v[k] * x[A->ci[k]];
-      lane[l] = p;
+      for (int64_t k = q + g; k < e; k += 8) p = p + A->v[k] * x[A->ci[k]];
+      lane[g] = p;
     }
-    y = y + tree64(lane);
+    for (int h = 1; h < 8; h <<= 1) {
+      for (int g = 0; g < 8; ++g) nx[g] = lane[g] + lane[g ^ h];
+      memcpy(lane, nx, sizeof(nx));
+    }
+    y = y + lane[0];
     q = e;
   }
   return y;
@@ -129,9 +135,8 @@ static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
 
 /* ------------------------------------------------------------ dot / norm */
 /* alpha = v . w in device order: short chunk c -> partial c (thread t owns short
- * positions CHUNK*c + t + 256q, fma accumulation, tree256); long group g ->
- * partial n_chunks + g (thread 64w accumulates fma over long rows 16g + w + 4i,
- * i = 0..3); then reduce_partials. */
+ * positions CHUNK*c + t + 256q, fma accumulation, tree256); long row r -> partial
+ * n_chunks + r = round(v * w); then reduce_partials over all of them. */
 static double dot_canon(const osched* S, const double* v, const double* w, double* P) {
   double acc[TPB];
   const int32_t nch = (S->n_short + CHUNK - 1) / CHUNK;
@@ -145,17 +150,8 @@ static double dot_canon(const osched* S, const double* v, const double* w, doubl
     }
     P[c] = tree256(acc);
   }
-  const int32_t ng = (S->n_long + GROUP - 1) / GROUP;
-  for (int32_t g = 0; g < ng; ++g) {
-    for (int t = 0; t < TPB; ++t) acc[t] = 0.0;
-    for (int wv = 0; wv < 4; ++wv)
-      for (int i = 0; i < GROUP / 4; ++i) {
-        const int32_t ri = g * GROUP + wv + 4 * i;
-        if (ri < S->n_long) acc[64 * wv] = fma(v[S->lrows[ri]], w[S->lrows[ri]], acc[64 * wv]);
-      }
-    P[nch + g] = tree256(acc);
-  }
-  return reduce_partials(P, nch + ng);
+  for (int32_t r = 0; r < S->n_long; ++r) P[nch + r] = v[S->lrows[r]] * w[S->lrows[r]];
+  return reduce_partials(P, nch + S->n_long);
 }
 static double dot_faithful(int64_t n, const double* v, const double* w) {
   double s = 0.0;

@@ -1,0 +1,46 @@
+"""Timeline of one SpMV-shaped launch from a TPL_STAMP build (dev tool). Marks per
+workgroup: [0] start, [1] scale known, [2] products staged / row sums, [3] piece sums
+staged, [4] publish drained, [5] end."""
+import os, sys, ctypes
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "two-pass-lanczos_amd"))
+import numpy as np
+import tpl_amd
+from tpl_amd import _lib
+from tpl_amd.utils.data_loader import load_kkt_system, write_qfc_3line
+K = 6
+write_qfc_3line("/tmp/t.qfc", 500000)
+a = load_kkt_system(os.path.join(ROOT, "tests/golden/kkt/netgen-500000-3.dmx.xz"), "/tmp/t.qfc").a
+n = a.shape[0]
+b = a @ np.full(n, 1 / np.sqrt(n))
+op = tpl_amd.HipCsrOp(a)
+tpl_amd.lanczos_two_pass(op, b, 50, "inv")
+sch = op.schedule()
+ns = len(sch["short_rows"])
+CR = int(os.environ.get("CR", "512"))
+nch = (ns + CR - 1) // CR
+fn = _lib.lib.tpl_debug_stamps
+fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
+def q(x):
+    x = x[np.isfinite(x)]
+    return " ".join(f"{v:6.2f}" for v in np.percentile(x, [0, 50, 90, 100])) if len(x) else "-"
+for kid, name in [(3, "spmv"), (2, "p2_spmv"), (0, "p1_spmv")]:
+    op.profile_kernel(kid, 20)
+    st = np.zeros(K * 65536, dtype=np.uint64)
+    fn(st.ctypes.data, 65536)
+    G = int(np.count_nonzero(st[0::K]))
+    nsl = G - nch
+    m = st[:K * G].reshape(G, K).astype(np.float64)
+    m[m == 0] = np.nan
+    base = np.nanmin(m[:, 0])
+    t = (m - base) / 100.0  # us
+    first = os.environ.get("FIRST", "slices")
+    ch, sl = (slice(0, nch), slice(nch, G)) if first == "chunks" else (slice(nsl, G), slice(0, nsl))
+    print(f"== {name}: grid {G} (chunks {nch}, bins {nsl}); us; pct 0/50/90/100")
+    for nm, sel, marks in [("chunk", ch, [1, 2]), ("bin", sl, [1, 2, 3, 4])]:
+        tt = t[sel]
+        print(f"  {nm:5s} start      {q(tt[:,0])}")
+        for k in marks:
+            print(f"  {nm:5s} mark{k}-start {q(tt[:,k]-tt[:,0])}")
+        print(f"  {nm:5s} end        {q(tt[:,5])} | dur {q(tt[:,5]-tt[:,0])}")
+    # stale marks from earlier launches are possible for marks a block did not reach

@@ -83,15 +83,26 @@ def md5_of_xz(path):
     return h.hexdigest()
 
 
-def canon_schedule(a, short_row_max=32, max_g2=1024):
+def short_row_threshold(lens, requested=-1):
+    """tpl_runtime.cpp short_row_threshold: clamp(2 * lower-median row nnz, 4, 32)."""
+    if requested > 0:
+        return requested
+    if lens.size == 0:
+        return 32
+    m = int(np.sort(np.minimum(lens, 33))[(lens.size + 1) // 2 - 1])
+    return max(4, min(32, 2 * m))
+
+
+def canon_schedule(a, short_row_max=-1, max_g2=1024):
     """The device's layout rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp, build_layout)
     restated, for oracle runs without a GPU. The GPU tests take the layout from the
     live operator instead (HipCsrOp.schedule())."""
     rp = a.indptr
     n = a.shape[0]
     lens = np.diff(rp)
-    short = np.nonzero(lens <= short_row_max)[0].astype(np.int32)
-    long_ = np.nonzero(lens > short_row_max)[0].astype(np.int32)
+    T = short_row_threshold(lens, short_row_max)
+    short = np.nonzero(lens <= T)[0].astype(np.int32)
+    long_ = np.nonzero(lens > T)[0].astype(np.int32)
     g2 = max(1, min(max_g2, -(-n // 1024)))
     per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)

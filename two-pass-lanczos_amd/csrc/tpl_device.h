@@ -3,33 +3,41 @@
 // these structs by value as kernel arguments.
 //
 // SpMV layout (built once per operator, tpl_runtime.cpp build_layout):
-//   * SHORT rows (<= kShortRowMax nnz), taken in ascending order, are stored as
-//     sliced ELL: chunk c holds short-row positions [C*c, C*c + C) (C = kChunkRows);
-//     entry k of position p sits at chunk_base[c] + k*C + (p - C*c) (column-major
-//     inside the chunk, padded to the chunk's widest row with col = -1). One workgroup
-//     per chunk, thread t owns positions C*c + t + 256q: every CSR load is coalesced
-//     and no row pointer is chased. When every chunk has the same width and the
-//     short rows are exactly rows 0..n_short-1 (the KKT arc block), chunk bases and
-//     row indices are computed, not loaded.
-//   * LONG rows are cut into kSlices column slices [n*s/8, n*(s+1)/8); a SLICE unit =
-//     (group g of 16 long rows, slice s): wave w walks rows 16g + w + 4i (i = 0..3),
-//     handled by workgroup n_chunks + 8g + s of the SpMV grid (chunks first) — under
-//     the observed round-robin dispatch each XCD's L2 then only caches 1/8 of the
-//     gathered vector (speed only, never correctness). Each unit publishes its 4 partials write-through (sc1) and bumps
-//     the group's counter; the 8th arriver sums the partials and runs the long rows'
-//     epilogue (split-K "last arriver" hand-off, cdna_hip_programming.md G16).
+//   * SHORT rows (<= T nnz, T = clamp(2 * median row nnz, 4, kShortRowMax) unless
+//     set explicitly), taken in ascending order, are stored as sliced ELL: chunk c
+//     holds short-row positions [C*c, C*c + C) (C = kChunkRows); entry k of position
+//     p sits at chunk_base[c] + k*C + (p - C*c) (column-major inside the chunk,
+//     padded to the chunk's widest row with col = -1). One workgroup per chunk,
+//     thread t owns positions C*c + t + 256q: every load is coalesced and no row
+//     pointer is chased. When every chunk has the same width W the chunk bases are
+//     computed, not loaded, and the kernel is specialised for W.
+//   * LONG rows are cut into kSlices column slices [floor(n*s/8), floor(n*(s+1)/8)).
+//     The (row, slice) pieces of slice s, long rows ascending, are packed whole into
+//     BINS of bin_cap entries (padding col = -1) with at most kBinSegs pieces each;
+//     every slice gets the same number M of bins. Bin m of slice s is workgroup
+//     8m + s of the slice part of the grid: under the round-robin dispatch of
+//     workgroups to XCDs all bins of a slice run on one XCD, whose L2 then only
+//     caches 1/8 of the gathered vector (speed only, never correctness). A bin's
+//     entries are read at computed addresses (thread t: entries t + 256u), the
+//     products are staged in LDS, and each piece is summed by 8 lanes. Every piece
+//     sum is published write-through into the row's slot (slots hold a sentinel
+//     while empty); after its store drains, the publisher reads the row's eight
+//     slots, and the one that sees all eight filled finalises the row (sums the
+//     slots, runs the epilogue, empties the slots). Nobody waits on anybody.
 //
 // Canonical reduction order (reproduced bit for bit by oracle/lanczos_oracle.c):
-//   * tree256(a[256])  : per 64-lane wave an xor butterfly (offsets 32,16,8,4,2,1,
+//   * tree256(a[256])  : per 64-lane wave an xor butterfly (offsets 1,2,4,8,16,32,
 //                        a_l <- a_l + a_{l^off}), then (S0 + S1) + (S2 + S3).
 //   * partials(P[N])   : thread t: s_t = 0; s_t += P[t + 256q] (q ascending); tree256.
 //   * short row        : s = 0; s += round(a_k x_k), k ascending.
-//   * long row         : per slice s: lane l: p_l = 0; p_l += round(a_k x_k) for
-//                        k = off[s] + l + 64q; P[s] = butterfly64(p); y = 0; y += P[s], s = 0..7.
-//   * alpha partial    : SHORT chunk c -> Pa[c]: thread t: acc = fma(v, w, acc) over its
+//   * long row         : per slice s: lane g (0..7): p_g = 0; p_g += round(a_k x_k) for
+//                        the slice's entries k = g + 8q (q ascending); P_s = xor
+//                        butterfly of p over 8 lanes (offsets 1, 2, 4); y = 0; y += P_s,
+//                        s = 0..7.
+//   * alpha partials   : Pa[c] (short chunk c): thread t: acc = fma(v, w, acc) over its
 //                        positions kChunkRows*c + t + 256q (q ascending), tree256;
-//                        long group g -> Pa[n_chunks + g]: thread 64w: acc = fma(v, w, acc)
-//                        over long rows 16g + w + 4i (i = 0..3), all others 0, tree256.
+//                        Pa[n_chunks + r] (long row r) = round(v * w).
+//                        alpha = partials(Pa[0 .. n_chunks + n_long)).
 //   * norm partial     : workgroup b (of G2) owns [bE, min(n,(b+1)E)); thread t visits
 //                        i0 = bE + 2t + 512q, then i0, i0+1: acc = fma(x,x,acc); tree256.
 #pragma once
@@ -39,44 +47,52 @@ namespace tpl {
 
 constexpr int kTPB = 256;            // threads per workgroup (4 waves of 64)
 #ifndef TPL_CHUNK_ROWS
-#define TPL_CHUNK_ROWS 256
+#define TPL_CHUNK_ROWS 512
 #endif
 constexpr int kChunkRows = TPL_CHUNK_ROWS; // short-row positions per SELL chunk
 constexpr int kRowsPerThread = kChunkRows / kTPB;
-constexpr int kShortRowMax = 32;     // rows with more nnz are "long" (sliced)
+constexpr int kShortRowMax = 32;     // upper bound of the short-row threshold
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
-#ifndef TPL_LONG_ROWS_PER_WAVE
-#define TPL_LONG_ROWS_PER_WAVE 4
+constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB table slots)
+#ifndef TPL_BIN_MIN
+#define TPL_BIN_MIN 2048
 #endif
-constexpr int kLongRowsPerWave = TPL_LONG_ROWS_PER_WAVE;  // long rows a wave walks in turn
-constexpr int kLongRowsPerGroup = 4 * kLongRowsPerWave;    // long rows per slice unit
+constexpr int kBinMin = TPL_BIN_MIN; // default entries per bin (8 per thread)
+constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
+// Slice partial slots hold this signalling-NaN bit pattern while empty (arithmetic
+// never produces a signalling NaN, so a published partial can never equal it).
+constexpr unsigned long long kSliceSentinel = 0x7FF0DEAD0BADF00DULL;
 constexpr double kBreakdownTol = 2.220446049250313080847263336181640625e-13; // 1000*f64::EPSILON, src/algorithms/mod.rs:140-143
+
+// One bin-table slot: piece start (offset in the bin), long-row index, global row.
+// Slot j < pieces describes piece j (its end is slot j+1's start); the slot after
+// the last piece holds the bin's fill with ri = row = -1, and so do all later slots.
+struct BinSeg {
+  int32_t start, ri, row, pad;
+};
 
 // Device view of the operator plus its layout.
 struct CsrDev {
-  // long rows: CSR (global arrays, only long rows' entries are read)
-  const int32_t* row_ptr;   // n+1 (int32: nnz < 2^31)
-  const int32_t* col;       // nnz
-  const double* val;        // nnz
-  const int32_t* lrows;     // n_long long-row indices (ascending)
-  const int32_t* loff;      // n_long x (kSlices+1) slice offsets into col/val
-  double* P;                // n_long x kSlices slice partials (sc1 hand-off)
-  int32_t* cnt;             // n_groups arrival counters (zero between launches)
   // short rows: sliced ELL
   const int32_t* srows;     // n_short short-row indices (ascending); unused if s_identity
   const int32_t* s_col;     // padded entries (col = -1 for padding)
   const double* s_val;
   const int32_t* c_base;    // n_chunks chunk base offsets; unused if s_width > 0
   const int32_t* c_width;   // n_chunks chunk widths; unused if s_width > 0
+  // long rows: bins (bin b = 8m + s holds pieces of slice s)
+  const int32_t* b_col;     // n_bins x bin_cap entries (col = -1: padding)
+  const double* b_val;
+  const BinSeg* b_seg;      // n_bins x kTPB table slots
+  double* P;                // n_long x kSlices piece partials (sentinel when empty)
   int32_t s_width;          // > 0: every chunk has this width (bases computed)
   int32_t s_identity;       // 1: short rows are exactly 0 .. n_short-1
   int32_t n_short;
   int32_t n_chunks;
   int32_t n_long;
-  int32_t n_groups;         // ceil(n_long / kLongRowsPerGroup)
-  int32_t n_slice_blocks;   // kSlices * n_groups; SpMV grid = n_chunks + n_slice_blocks
+  int32_t bin_cap;          // entries per bin (multiple of kTPB)
+  int32_t n_slice_blocks;   // kSlices * M; SpMV grid = n_chunks + n_slice_blocks
   int32_t G2;               // workgroups of the element-wise kernels == #norm partials
-  int32_t NA;               // #alpha partials = n_chunks + n_groups
+  int32_t NA;               // #alpha partials = n_chunks + n_long
   int32_t pad;
   int64_t n;
   int64_t E;                // elements per workgroup of the element-wise kernels

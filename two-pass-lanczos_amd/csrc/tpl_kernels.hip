@@ -21,32 +21,85 @@
 //   regenerates pass one's basis bit for bit (reference: basis_drift_fro = 0.0,
 //   results/orthogonality_*.csv).
 //
-// Latency structure (measured: a graph-launched empty kernel costs 1.6 us and each
-// dependent round of random gathers ~1.9 us on MI355X): every workgroup issues its
-// independent loads (stop flag, grid partials, CSR entries, epilogue vectors)
-// before its first wait, so a short-row chunk costs two memory round trips
-// (entries -> gathers) and the grid-reduction prologue hides under them.
+// Latency structure (measured on MI355X: a graph-launched empty kernel costs 1.6 us,
+// and a dependent memory round trip 1-2 us once the chip is loaded): every
+// workgroup issues its independent loads (stop flag, grid partials, entries,
+// epilogue vectors) before its first wait. A short-row chunk costs two round trips
+// (entries -> gathers); a long-row bin the same two plus an LDS pass, and the
+// slice-7 bins one more (polling the other slices' partials).
 #include <hip/hip_runtime.h>
 #include "tpl_device.h"
 
 // Performance-ablation switches for experiments only (scripts/ablate.sh builds
 // separate libraries); production builds have TPL_ABLATE == 0. Bit 1: skip the
-// slice units; 2: skip the short chunks; 4: no last-arriver hand-off.
+// long-row bins; 2: skip the short chunks; 4: skip the bins' piece sums.
 #ifndef TPL_ABLATE
 #define TPL_ABLATE 0
 #endif
 
 namespace tpl {
 
+#ifndef TPL_STAMP
+#define TPL_STAMP 0
+#endif
+#if TPL_STAMP
+// Diagnostic builds only: per-workgroup s_memrealtime (100 MHz) marks of the most
+// recent SpMV-shaped launch — [0] start, [1] scale known, [2] products staged /
+// row sums done, [3] piece sums staged, [4] publish drained, [5] end — read back
+// by tpl_debug_stamps().
+constexpr int kMarks = 6;
+__device__ unsigned long long g_stamps[kMarks * 65536];
+#define TPL_MARK(k)                                                          \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 65536)                              \
+      g_stamps[kMarks * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define TPL_MARK(k) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------- reductions
+// 64-bit lane exchange through a DPP pattern (two 32-bit moves).
+template <int kCtrl>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, kCtrl, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), kCtrl, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double swz_xor16_f64(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)b, 0x401F);  // bitmode: xor 16 within 32
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// Sum over the 64 lanes of a wave (all lanes active), as the xor butterfly with
+// offsets 1, 2, 4, 8, 16, 32: lane l <- a_l + a_{l^h}. Once a stage is done every
+// group of 2h lanes holds one value, so any exchange pairing a group with its
+// partner group gives the same bits (IEEE addition is commutative); that lets the
+// stages run on DPP (quad_perm, half-row and row mirrors), one swizzle and a
+// readlane instead of LDS permutes. Every lane returns the same, order-fixed value.
 __device__ __forceinline__ double wave_sum(double v) {
-  // xor butterfly: every lane ends with the same, order-fixed value.
-  v = v + __shfl_xor(v, 32);
-  v = v + __shfl_xor(v, 16);
-  v = v + __shfl_xor(v, 8);
-  v = v + __shfl_xor(v, 4);
-  v = v + __shfl_xor(v, 2);
-  v = v + __shfl_xor(v, 1);
+  v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
+  v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
+  v = v + dpp_f64<0x141>(v);  // row_half_mirror: partner quad in the 8-lane group
+  v = v + dpp_f64<0x140>(v);  // row_mirror: partner 8-lane group in the row
+  v = v + swz_xor16_f64(v);   // xor 16
+  return readlane_f64(v, 0) + readlane_f64(v, 32);
+}
+
+// Sum over each aligned group of 8 lanes (butterfly offsets 1, 2, 4), all on DPP.
+__device__ __forceinline__ double group8_sum(double v) {
+  v = v + dpp_f64<0xB1>(v);   // xor 1
+  v = v + dpp_f64<0x4E>(v);   // xor 2
+  v = v + dpp_f64<0x141>(v);  // partner quad in the 8-lane group
   return v;
 }
 
@@ -62,25 +115,29 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
 }
 
 // Issue the partial loads (independent) early ...
+template <int R>
 struct PartialRegs {
-  double v[8];
+  double v[R];
 };
 // (Every load below is unconditional with a clamped index and its result masked
 // afterwards: a load under a runtime condition makes hipcc branch around it and
 // drain vmcnt per element, serialising the round trips — guide §5 trap (c).)
 __device__ __forceinline__ int clampi(int i, int hi) { return i < hi ? i : hi; }
-__device__ __forceinline__ void load_partials(const double* __restrict__ P, int N, PartialRegs& r) {
+template <int R>
+__device__ __forceinline__ void load_partials(const double* __restrict__ P, int N,
+                                              PartialRegs<R>& r) {
 #pragma unroll
-  for (int u = 0; u < 8; ++u) r.v[u] = P[clampi(threadIdx.x + u * kTPB, N - 1)];
+  for (int u = 0; u < R; ++u) r.v[u] = P[clampi(threadIdx.x + u * kTPB, N - 1)];
 }
 // ... and reduce them later in the canonical order (s = 0; s += P[t + 256q]).
+template <int R>
 __device__ __forceinline__ double finish_partials(const double* __restrict__ P, int N,
-                                                  const PartialRegs& r, double* red) {
+                                                  const PartialRegs<R>& r, double* red) {
   double s = 0.0;
 #pragma unroll
-  for (int u = 0; u < 8; ++u)
+  for (int u = 0; u < R; ++u)
     if ((int)threadIdx.x + u * kTPB < N) s = s + r.v[u];
-  for (int i = threadIdx.x + 8 * kTPB; i < N; i += kTPB) s = s + P[i]; // N > 2048 (rare)
+  for (int i = threadIdx.x + R * kTPB; i < N; i += kTPB) s = s + P[i]; // N > 256 R (rare)
   return block_sum(s, red);
 }
 
@@ -92,6 +149,7 @@ struct EpiSpmv {
   double* y;
   __device__ __forceinline__ PreNone pre(int) const { return {}; }
   __device__ __forceinline__ void apply(int i, double s, const PreNone&, double&) const { y[i] = s; }
+  __device__ __forceinline__ void long_alpha(int, double) const {}
 };
 
 // pass one / standard: w = y - beta_{j-1} v_{j-1}; alpha partial += v_j . w
@@ -105,7 +163,10 @@ struct EpiPass1 {
   double invN_cur, invN_prev, beta_sub;
   double* W;
   double* Vcol;         // standard variant: column j-1 of V_k, else nullptr
+  double* Pa_long;      // alpha partials of the long rows (Pa + n_chunks)
   __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
+  // long row r: its alpha partial is the single rounded product v * w
+  __device__ __forceinline__ void long_alpha(int r, double acc) const { Pa_long[r] = acc; }
   __device__ __forceinline__ void apply(int i, double s, const Pre1& p, double& acc) const {
     const double v = p.rc * invN_cur;
     const double vp = has_prev ? p.rp * invN_prev : 0.0;
@@ -138,6 +199,7 @@ struct EpiPass2 {
     x[i] = p.x + ycoef * vn;
     if (Vcol) Vcol[i] = vn;
   }
+  __device__ __forceinline__ void long_alpha(int, double) const {}
 };
 
 // Result of a workgroup's prologue: the gather scale, or "stop" (uniform across the grid).
@@ -184,6 +246,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 #pragma unroll
     for (int k = 0; k < W; ++k) xv[q][k] = xsrc[c[q][k] < 0 ? 0 : c[q][k]];
   const Scale sc = scale_of();
+  TPL_MARK(1);
   if (!sc.ok) return false; // stopped / breakdown (uniform)
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) {
@@ -195,59 +258,58 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
     }
     if (live[q]) epi.apply(row[q], sum, pre[q], acc);
   }
+  TPL_MARK(2);
   return true;
 }
 
-// Any width: entries in batches of 4 per row.
+// Any width (rare: chunks wider than 4). One row position at a time, entries in
+// batches of 8 with every load of a batch in flight; kept lean in registers, since a
+// kernel's VGPR budget is the maximum over all of its paths.
 template <class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int base, int W,
                                                 const double* __restrict__ xsrc, ScaleFn scale_of,
                                                 const Epi& epi, double& acc) {
   const int t = threadIdx.x;
-  int row[kRowsPerThread];
-  bool live[kRowsPerThread];
-  decltype(epi.pre(0)) pre[kRowsPerThread];
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    const int p = chunk * kChunkRows + q * kTPB + t;
-    live[q] = p < A.n_short;
-    const int pc = clampi(p, A.n_short - 1);
-    row[q] = A.s_identity ? pc : A.srows[pc];
-  }
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
   const Scale sc = scale_of();
   if (!sc.ok) return false;
-  double s[kRowsPerThread];
+#pragma unroll 1
+  for (int q = 0; q < kRowsPerThread; ++q) {
+    const int p = chunk * kChunkRows + q * kTPB + t;
+    const bool live = p < A.n_short;
+    const int pc = clampi(p, A.n_short - 1);
+    const int row = A.s_identity ? pc : A.srows[pc];
+    const auto pre = epi.pre(row);
+    double s = 0.0;
+#pragma unroll 1
+    for (int k0 = 0; k0 < W; k0 += 8) {
+      int c[8];
+      double a[8], xv[8];
 #pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) s[q] = 0.0;
-  for (int k = 0; k < W; ++k) {
-    int c[kRowsPerThread];
-    double a[kRowsPerThread], xv[kRowsPerThread];
+      for (int u = 0; u < 8; ++u) {
+        const int e = base + clampi(k0 + u, W - 1) * kChunkRows + q * kTPB + t;
+        c[u] = A.s_col[e];
+        a[u] = A.s_val[e];
+      }
 #pragma unroll
-    for (int q = 0; q < kRowsPerThread; ++q) {
-      const int e = base + k * kChunkRows + q * kTPB + t;
-      c[q] = A.s_col[e];
-      a[q] = A.s_val[e];
+      for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const double nxt = s + a[u] * (xv[u] * sc.s);
+        s = (c[u] >= 0 && k0 + u < W) ? nxt : s;
+      }
     }
-#pragma unroll
-    for (int q = 0; q < kRowsPerThread; ++q) xv[q] = xsrc[c[q] < 0 ? 0 : c[q]];
-#pragma unroll
-    for (int q = 0; q < kRowsPerThread; ++q) {
-      const double nxt = s[q] + a[q] * (xv[q] * sc.s);
-      s[q] = c[q] >= 0 ? nxt : s[q];
-    }
+    if (live) epi.apply(row, s, pre, acc);
   }
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q)
-    if (live[q]) epi.apply(row[q], s[q], pre[q], acc);
   return true;
 }
 
-template <class Epi, class ScaleFn>
+// CW > 0: the kernel was specialised for a uniform chunk width CW (tpl::launch picks
+// it from A.s_width); CW == 0: generic, any per-chunk width.
+template <int CW, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
                                             const double* __restrict__ xsrc, ScaleFn scale_of,
                                             const Epi& epi, double& acc) {
+  if (CW > 0) return short_chunk_w<CW>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
   int W, base;
   if (A.s_width > 0) {
     W = A.s_width;
@@ -265,153 +327,155 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
   }
 }
 
-// -------------------------------------------------------- long rows (slices)
-// Slice unit (group g of 16 long rows, slice s): wave w walks rows 16g + w + 4i.
-// Returns 1 in the workgroup that finalised the group (the 8th arriver; its thread
-// 64w applied the epilogue of its rows, acc updated), 0 otherwise, -1 if stopped.
+// ------------------------------------------------------ long rows (bins)
+// Bin m of slice s. Thread t loads entries t + 256u of the bin (coalesced, at
+// computed addresses) and its bin-table slot; the products go to LDS; each piece is
+// then summed by one wave (lane-strided + butterfly) and handed back to thread j,
+// which owns piece j and publishes it; whoever completes a row's eight finalises it.
+// lds: bin_cap doubles of products, kTPB ints of piece starts, kTPB piece sums.
 template <class Epi, class ScaleFn>
-__device__ __forceinline__ int slice_unit(const CsrDev& A, int g, int s,
-                                          const double* __restrict__ xsrc, ScaleFn scale_of,
-                                          const Epi& epi, double& acc, int* lds_flag) {
-  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  int ri[kLongRowsPerWave], row[kLongRowsPerWave], b[kLongRowsPerWave], e[kLongRowsPerWave];
-  bool live[kLongRowsPerWave];
-  decltype(epi.pre(0)) pre[kLongRowsPerWave];
+__device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
+                                         const double* __restrict__ xsrc, ScaleFn scale_of,
+                                         const Epi& epi, double* lds) {
+  const int t = threadIdx.x;
+  const int bin = m * kSlices + s;
+  const BinSeg sg = A.b_seg[bin * kTPB + t];
+  const int base = bin * A.bin_cap;
+  int c[8];
+  double a[8], xv[8];
 #pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i) {
-    ri[i] = g * kLongRowsPerGroup + w + 4 * i;
-    live[i] = ri[i] < A.n_long;
-    const int ric = clampi(ri[i], A.n_long - 1);
-    b[i] = A.loff[ric * (kSlices + 1) + s];
-    e[i] = A.loff[ric * (kSlices + 1) + s + 1];
-    row[i] = A.lrows[ric];
-    if (!live[i]) e[i] = b[i];
+  for (int u = 0; u < 8; ++u) {
+    c[u] = A.b_col[base + u * kTPB + t];
+    a[u] = A.b_val[base + u * kTPB + t];
   }
 #pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i) pre[i] = epi.pre(row[i]); // finaliser only
-  // first batch: 2 entries per lane of every row, issued before the scale is known
-  int c0[kLongRowsPerWave][2];
-  double a0[kLongRowsPerWave][2], x0[kLongRowsPerWave][2];
-#pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int k = clampi(b[i] + lane + 64 * u, e[i] > b[i] ? e[i] - 1 : b[i]);
-      c0[i][u] = A.col[k];
-      a0[i][u] = A.val[k];
-    }
-#pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) x0[i][u] = xsrc[c0[i][u]];
+  for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
+  // the finalising thread's own row entries travel with the gathers
+  const auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
   const Scale sc = scale_of();
-  if (!sc.ok) return -1; // stopped / breakdown (uniform): counters untouched
-  const double scale = sc.s;
-  double p[kLongRowsPerWave];
+  TPL_MARK(1);
+  if (!sc.ok) return; // stopped / breakdown (uniform): slots untouched
 #pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i) {
-    p[i] = 0.0;
+  for (int u = 0; u < 8; ++u) lds[u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
+  for (int u0 = 8 * kTPB; u0 < A.bin_cap; u0 += 8 * kTPB) { // bins wider than 2048 (rare)
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const double nxt = p[i] + a0[i][u] * (x0[i][u] * scale);
-      p[i] = (b[i] + lane + 64 * u < e[i]) ? nxt : p[i];
+    for (int u = 0; u < 8; ++u) {
+      c[u] = A.b_col[base + u0 + u * kTPB + t];
+      a[u] = A.b_val[base + u0 + u * kTPB + t];
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      lds[u0 + u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
   }
-  // remaining entries, 4 per lane per batch
+  int* starts = reinterpret_cast<int*>(lds + A.bin_cap);
+  double* psum = lds + A.bin_cap + kTPB / 2;  // kTPB doubles after the starts
+  starts[t] = sg.ri < 0 ? -1 - sg.start : sg.start;  // < 0: no piece (value encodes the fill)
+  const int npieces = __syncthreads_count(sg.ri >= 0);  // pieces are a prefix of the table
+  TPL_MARK(2);
+  // Piece sums, 32 pieces per pass: the 8-lane group t >> 3 takes piece j0 + (t >> 3);
+  // its lane g sums the piece's entries g + 8q, then a butterfly over the 8 lanes
+  // (canonical long-row order).
+  const int g8 = t & 7;
+  for (int j0 = 0; j0 < npieces; j0 += kTPB / 8) {
+    const int j = j0 + (t >> 3);
+    const int jc = j < kTPB - 2 ? j : kTPB - 2;
+    const int st = starts[jc], nx = starts[jc + 1];
+    const bool valid = j < npieces;
+    const int b0 = valid ? st : 0;
+    const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
+    double acc = 0.0;
+    if (!(TPL_ABLATE & 4)) {
+      for (int k0 = b0 + g8; k0 < en; k0 += 64) {  // 8 reads in flight, then the adds
+        double v[8];
 #pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i) {
-    const int last_e = e[i] > b[i] ? e[i] - 1 : b[i];
-    for (int q = b[i] + lane + 128; q < e[i]; q += 256) {
-      int c[4];
-      double a[4], xv[4];
+        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = clampi(q + 64 * u, last_e);
-        c[u] = A.col[k];
-        a[u] = A.val[k];
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) xv[u] = xsrc[c[u]];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const double nxt = p[i] + a[u] * (xv[u] * scale);
-        p[i] = (q + 64 * u < e[i]) ? nxt : p[i];
+        for (int u = 0; u < 8; ++u) acc = k0 + 8 * u < en ? acc + v[u] : acc;
       }
     }
+    acc = group8_sum(acc);
+    if (g8 == 0 && valid) psum[j] = acc;
   }
-#pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i) p[i] = wave_sum(p[i]);
-  if (TPL_ABLATE & 4) {
-#pragma unroll
-    for (int i = 0; i < kLongRowsPerWave; ++i)
-      if (live[i] && lane == 0) A.P[ri[i] * kSlices + s] = p[i];
-    return 0;
-  }
-  // Publish write-through (sc1), drain, count arrivals (split-K last-arriver form).
-#pragma unroll
-  for (int i = 0; i < kLongRowsPerWave; ++i)
-    if (live[i] && lane == 0)
-      __hip_atomic_store(&A.P[ri[i] * kSlices + s], p[i], __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  TPL_MARK(3);
+  if (sg.ri < 0) return; // no piece for this thread
+  const double p = psum[t];
+  // Hand-off, data-tagged: publish the piece sum write-through, drain, then read the
+  // row's eight slots. The publisher whose store completed last sees all eight, so
+  // some thread always finalises; a tie finalises twice, writing identical bits
+  // (every input — the slots, the row's vector entries loaded before publishing — is
+  // the same). No thread ever waits on another: nothing depends on dispatch order.
+  unsigned long long* slots = reinterpret_cast<unsigned long long*>(A.P + (size_t)sg.ri * kSlices);
+  __hip_atomic_store(slots + s, (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int old = __hip_atomic_fetch_add(&A.cnt[g], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *lds_flag = (old == kSlices - 1);
-  }
-  __syncthreads();
-  const int last = *lds_flag;
-  if (last) {
-    if (threadIdx.x == 0)
-      __hip_atomic_store(&A.cnt[g], 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); // next launch
-    if (lane == 0) {
-      double ps[kLongRowsPerWave][kSlices];
+  TPL_MARK(4);
+  unsigned long long v[kSlices];
 #pragma unroll
-      for (int i = 0; i < kLongRowsPerWave; ++i)
+  for (int k = 0; k < kSlices; ++k)
+    v[k] = __hip_atomic_load(slots + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool all = true;
 #pragma unroll
-        for (int k = 0; k < kSlices; ++k)
-          ps[i][k] = __hip_atomic_load(&A.P[clampi(ri[i], A.n_long - 1) * kSlices + k],
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < kSlices; ++k) all = all && v[k] != kSliceSentinel;
+  if (!all) return;
 #pragma unroll
-      for (int i = 0; i < kLongRowsPerWave; ++i) {
-        double y = 0.0;
+  for (int k = 0; k < kSlices; ++k)  // empty again for the next launch
+    __hip_atomic_store(slots + k, kSliceSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double y = 0.0;
 #pragma unroll
-        for (int k = 0; k < kSlices; ++k) y = y + ps[i][k];
-        if (live[i]) epi.apply(row[i], y, pre[i], acc);
-      }
-    }
-  }
-  return last;
+  for (int k = 0; k < kSlices; ++k) y = y + __longlong_as_double((long long)v[k]);
+  double acc = 0.0;
+  epi.apply(sg.row, y, pre, acc);
+  epi.long_alpha(sg.ri, acc);
 }
 
-#ifndef TPL_CHUNKS_FIRST
-#define TPL_CHUNKS_FIRST 1
+// Minimum waves per SIMD requested for the SpMV-shaped kernels (occupancy vs VGPRs).
+#ifndef TPL_SPMV_MIN_WAVES
+#define TPL_SPMV_MIN_WAVES 1
 #endif
-template <class Epi, class ScaleFn>
-__device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
-                                          ScaleFn scale_of, const Epi& epi, double& acc,
-                                          int* lds_flag) {
+#ifndef TPL_CHUNKS_FIRST
+#define TPL_CHUNKS_FIRST 0
+#endif
+// Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
+// index whose alpha partial this workgroup owns, or -1.
+template <int CW, class Epi, class ScaleFn>
+__device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __restrict__ xsrc,
+                                               ScaleFn scale_of, const Epi& epi, double& acc,
+                                               double* lds) {
   int b = blockIdx.x;
-  if (TPL_CHUNKS_FIRST) { // [chunks][slices]: slice s of group g at n_chunks + 8g + s
-    b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
-  }
+  if (TPL_CHUNKS_FIRST) b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
   if (b < A.n_slice_blocks) {
-    if (TPL_ABLATE & 1) return -1;
-    const int g = b / kSlices;
-    const int last = slice_unit(A, g, b % kSlices, xsrc, scale_of, epi, acc, lds_flag);
-    return last == 1 ? A.n_chunks + g : -1;
+    if (!(TPL_ABLATE & 1)) long_bin(A, b / kSlices, b % kSlices, xsrc, scale_of, epi, lds);
+    return -1;
   }
   const int chunk = b - A.n_slice_blocks;
   if (TPL_ABLATE & 2) return -1;
-  return short_chunk(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
+  return short_chunk<CW>(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
+}
+
+template <int CW, class Epi, class ScaleFn>
+__device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
+                                          ScaleFn scale_of, const Epi& epi, double& acc,
+                                          double* lds) {
+#if TPL_STAMP
+  TPL_MARK(0);
+  const int r = spmv_block_impl<CW>(A, xsrc, scale_of, epi, acc, lds);
+  TPL_MARK(5);
+  return r;
+#else
+  return spmv_block_impl<CW>(A, xsrc, scale_of, epi, acc, lds);
+#endif
 }
 
 // ------------------------------------------------------------------ kernels
-__global__ __launch_bounds__(kTPB) void k_spmv(CsrDev A, const double* __restrict__ x,
+template <int CW>
+__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_spmv(CsrDev A, const double* __restrict__ x,
                                                double* __restrict__ y) {
-  __shared__ int lds_flag;
+  extern __shared__ double lds[];
   double acc = 0.0;
-  spmv_block(A, x, UnitScale{}, EpiSpmv{y}, acc, &lds_flag);
+  spmv_block<CW>(A, x, UnitScale{}, EpiSpmv{y}, acc, lds);
 }
 
 // Pass-one prologue: ||b||^2 partials, reset flags.
@@ -441,15 +505,16 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
 }
 
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1).
-__global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
+template <int CW>
+__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ r_cur,
                                                   const double* __restrict__ r_prev,
                                                   double* __restrict__ W,
                                                   double* __restrict__ Vcol, int j) {
   __shared__ double red[4];
-  __shared__ int lds_flag;
+  extern __shared__ double lds[];
   const int stop = S.flags[0]; // checked after the loads are in flight
-  PartialRegs pr;
+  PartialRegs<4> pr;           // G2 <= 1024
   load_partials(S.Pb, A.G2, pr);
   const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
   EpiPass1 epi;
@@ -461,6 +526,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
   epi.beta_sub = 0.0;
   epi.W = W;
   epi.Vcol = Vcol;
+  epi.Pa_long = S.Pa + A.n_chunks;
   // beta_{j-1} (||b|| at j = 1) from the norm partials; fills the epilogue.
   auto scale_fn = [&]() -> Scale {
     if (stop) return Scale{0.0, false};
@@ -484,7 +550,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_spmv(CsrDev A, DevState S,
     return Scale{epi.invN_cur, true};
   };
   double acc = 0.0;
-  const int slot = spmv_block(A, r_cur, scale_fn, epi, acc, &lds_flag);
+  const int slot = spmv_block<CW>(A, r_cur, scale_fn, epi, acc, lds);
   if (slot < 0) return; // uniform per workgroup
   const double p = block_sum(acc, red);
   if (threadIdx.x == 0) S.Pa[slot] = p;
@@ -497,7 +563,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   double* __restrict__ r_next, int j, int k) {
   __shared__ double red[4];
   const int stop = S.flags[0];
-  PartialRegs pr;
+  PartialRegs<12> pr;
   load_partials(S.Pa, A.NA, pr);
   const int64_t beg = (int64_t)blockIdx.x * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
@@ -562,13 +628,14 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
 }
 
 // Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x.
-__global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
+template <int CW>
+__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ v_cur,
                                                   const double* __restrict__ v_prev,
                                                   double* __restrict__ v_next,
                                                   double* __restrict__ x,
                                                   double* __restrict__ Vcol, int j) {
-  __shared__ int lds_flag;
+  extern __shared__ double lds[];
   EpiPass2 epi;
   epi.v_cur = v_cur;
   epi.v_prev = (j >= 2) ? v_prev : v_cur;
@@ -581,7 +648,7 @@ __global__ __launch_bounds__(kTPB) void k_p2_spmv(CsrDev A, DevState S,
   epi.x = x;
   epi.Vcol = Vcol;
   double acc = 0.0;
-  spmv_block(A, v_cur, UnitScale{}, epi, acc, &lds_flag);
+  spmv_block<CW>(A, v_cur, UnitScale{}, epi, acc, lds);
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
@@ -636,7 +703,7 @@ __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
 __global__ __launch_bounds__(kTPB) void k_reorth_reduce(const double* __restrict__ P, int G,
                                                         double* __restrict__ h) {
   __shared__ double red[4];
-  PartialRegs pr;
+  PartialRegs<8> pr;
   const double* Pc = P + (int64_t)blockIdx.x * G;
   load_partials(Pc, G, pr);
   const double s = finish_partials(Pc, G, pr, red);
@@ -684,9 +751,28 @@ static inline int elem_grid(int64_t n) {
   return (int)g;
 }
 static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + A.n_chunks; }
+// dynamic LDS of the SpMV-shaped kernels: a bin's staged products + piece starts
+static inline size_t spmv_lds_bytes(const CsrDev& A) {
+  return A.n_slice_blocks > 0
+             ? (size_t)A.bin_cap * sizeof(double) + kTPB * sizeof(int) + kTPB * sizeof(double)
+             : 0;
+}
+// Launch the SpMV-shaped kernel specialised for the layout's uniform chunk width.
+#define TPL_LAUNCH_CW(KERNEL, A, s, ...)                                                    \
+  do {                                                                                      \
+    const dim3 grid_(spmv_grid(A)), block_(kTPB);                                           \
+    const size_t shm_ = spmv_lds_bytes(A);                                                  \
+    switch ((A).s_width >= 1 && (A).s_width <= 4 ? (A).s_width : 0) {                       \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
+      case 2: hipLaunchKernelGGL(KERNEL<2>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
+      case 3: hipLaunchKernelGGL(KERNEL<3>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
+      case 4: hipLaunchKernelGGL(KERNEL<4>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
+      default: hipLaunchKernelGGL(KERNEL<0>, grid_, block_, shm_, s, __VA_ARGS__); break;   \
+    }                                                                                       \
+  } while (0)
 
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s) {
-  if (spmv_grid(A) > 0) hipLaunchKernelGGL(k_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, x, y);
+  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_spmv, A, s, A, x, y);
   return hipGetLastError();
 }
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s) {
@@ -695,9 +781,7 @@ hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStrea
 }
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
                    double* W, double* Vcol, int j, hipStream_t s) {
-  if (spmv_grid(A) > 0)
-    hipLaunchKernelGGL(k_p1_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, r_cur, r_prev, W,
-                       Vcol, j);
+  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, r_cur, r_prev, W, Vcol, j);
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
@@ -712,9 +796,7 @@ hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, do
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
                    double* v_next, double* x, double* Vcol, int j, hipStream_t s) {
-  if (spmv_grid(A) > 0)
-    hipLaunchKernelGGL(k_p2_spmv, dim3(spmv_grid(A)), dim3(kTPB), 0, s, A, S, v_cur, v_prev,
-                       v_next, x, Vcol, j);
+  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, v_cur, v_prev, v_next, x, Vcol, j);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
@@ -740,3 +822,9 @@ hipError_t reorth_update(int64_t n, int cols, const double* V, double* r, const 
 
 } // namespace launch
 } // namespace tpl
+
+#if TPL_STAMP
+extern "C" int tpl_debug_stamps(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps), sizeof(unsigned long long) * tpl::kMarks * n);
+}
+#endif

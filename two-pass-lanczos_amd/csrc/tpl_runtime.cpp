@@ -93,7 +93,7 @@ static tpl_status guarded(F&& f) {
 
 // ------------------------------------------------------------ layout
 struct SchedParams {
-  int short_row_max = kShortRowMax; // rows longer than this are sliced
+  int short_row_max = -1;           // rows longer than this are sliced; -1 = auto
   int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
 };
 
@@ -106,17 +106,43 @@ struct Layout {
   int32_t s_width = 0;              // uniform chunk width (0: per-chunk)
   int32_t s_identity = 0;
   std::vector<int32_t> lrows;       // long rows, ascending
-  std::vector<int32_t> loff;        // n_long x (kSlices + 1)
+  std::vector<int32_t> b_col;       // long-row bins: n_bins x bin_cap entries
+  std::vector<double> b_val;
+  std::vector<BinSeg> b_seg;        // n_bins x kTPB table slots
+  int32_t bin_cap = kBinMin;
+  int32_t M = 0;                    // bins per slice
   int G2 = 1;
   int64_t E = 512;
 };
+
+// Auto rule: T = clamp(2 * median row length, 4, kShortRowMax). A sliced-ELL chunk
+// costs as much as its widest row, so the few rows far above the typical length
+// (e.g. the short node rows of a KKT matrix) go to the sliced long-row path instead
+// of widening a chunk.
+static int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int requested) {
+  if (requested > 0) return requested;
+  if (n == 0) return kShortRowMax;
+  std::vector<int32_t> hist(kShortRowMax + 2, 0);
+  for (int64_t i = 0; i < n; ++i) hist[std::min<int32_t>(rp[i + 1] - rp[i], kShortRowMax + 1)]++;
+  int64_t seen = 0;
+  int32_t median = kShortRowMax + 1;
+  for (int32_t l = 0; l <= kShortRowMax + 1; ++l) {
+    seen += hist[l];
+    if (2 * seen >= n) {  // lower median
+      median = l;
+      break;
+    }
+  }
+  return std::max<int32_t>(4, std::min<int32_t>(kShortRowMax, 2 * median));
+}
 
 static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
                            const std::vector<int32_t>& col, const std::vector<double>& val,
                            const SchedParams& sp) {
   Layout L;
+  const int32_t T = short_row_threshold(n, rp, sp.short_row_max);
   for (int64_t i = 0; i < n; ++i) {
-    if (rp[i + 1] - rp[i] > sp.short_row_max) L.lrows.push_back((int32_t)i);
+    if (rp[i + 1] - rp[i] > T) L.lrows.push_back((int32_t)i);
     else L.srows.push_back((int32_t)i);
   }
   const int64_t ns = (int64_t)L.srows.size();
@@ -156,17 +182,68 @@ static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
     for (int64_t c = 0; c < nchunks; ++c) uni = uni && L.c_width[c] == L.c_width[0];
     if (uni && L.c_width[0] > 0) L.s_width = L.c_width[0];
   }
-  // slice offsets: first entry of long row r with column >= floor(n * s / kSlices)
-  L.loff.resize(L.lrows.size() * (kSlices + 1));
-  for (size_t r = 0; r < L.lrows.size(); ++r) {
+  // Long rows: piece (r, s) = entries of long row r with columns in slice s; the
+  // pieces of slice s, r ascending, are packed whole into bins (first fit in order).
+  const size_t nl = L.lrows.size();
+  std::vector<int32_t> poff(nl * (kSlices + 1));
+  int32_t widest = 0;
+  for (size_t r = 0; r < nl; ++r) {
     const int32_t row = L.lrows[r];
     int32_t q = rp[row];
     for (int s = 0; s <= kSlices; ++s) {
       const int64_t bound = n * s / kSlices;
       while (q < rp[row + 1] && col[q] < bound) ++q;
-      L.loff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
+      poff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
+      if (s > 0)
+        widest = std::max(widest, poff[r * (kSlices + 1) + s] - poff[r * (kSlices + 1) + s - 1]);
     }
   }
+  if (widest > kBinMax)
+    fail(TPL_ERR_UNSUPPORTED, "a long row has " + std::to_string(widest) +
+                                  " nonzeros in one of its 8 column slices (limit " +
+                                  std::to_string(kBinMax) + ")");
+  L.bin_cap = std::max<int32_t>(kBinMin, ((widest + kTPB - 1) / kTPB) * kTPB);
+  L.bin_cap = ((L.bin_cap + 8 * kTPB - 1) / (8 * kTPB)) * (8 * kTPB);  // whole load batches
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> bins[kSlices]; // (r, fill-at-start)
+  std::vector<int32_t> fill[kSlices];
+  for (int s = 0; s < kSlices && nl > 0; ++s) {
+    for (size_t r = 0; r < nl; ++r) {
+      const int32_t cnt = poff[r * (kSlices + 1) + s + 1] - poff[r * (kSlices + 1) + s];
+      if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
+          (int)bins[s].back().size() == kBinSegs) {
+        bins[s].emplace_back();
+        fill[s].push_back(0);
+      }
+      bins[s].back().emplace_back((int32_t)r, fill[s].back());
+      fill[s].back() += cnt;
+    }
+  }
+  L.M = 0;
+  for (int s = 0; s < kSlices; ++s) L.M = std::max<int32_t>(L.M, (int32_t)bins[s].size());
+  const size_t nbins = (size_t)kSlices * L.M;
+  L.b_col.assign(std::max<size_t>(nbins * L.bin_cap, 1), -1);
+  L.b_val.assign(std::max<size_t>(nbins * L.bin_cap, 1), 0.0);
+  L.b_seg.assign(std::max<size_t>(nbins * kTPB, 1), BinSeg{0, -1, -1, 0});
+  for (int s = 0; s < kSlices; ++s)
+    for (int32_t m = 0; m < L.M; ++m) {
+      const size_t bin = (size_t)m * kSlices + s;
+      int32_t f = 0;
+      if (m < (int32_t)bins[s].size()) {
+        const auto& pieces = bins[s][m];
+        for (size_t j = 0; j < pieces.size(); ++j) {
+          const int32_t r = pieces[j].first, start = pieces[j].second;
+          const int32_t q0 = poff[r * (kSlices + 1) + s], q1 = poff[r * (kSlices + 1) + s + 1];
+          L.b_seg[bin * kTPB + j] = BinSeg{start, r, L.lrows[r], 0};
+          for (int32_t q = q0; q < q1; ++q) {
+            L.b_col[bin * L.bin_cap + start + (q - q0)] = col[q];
+            L.b_val[bin * L.bin_cap + start + (q - q0)] = val[q];
+          }
+        }
+        f = fill[s][m];
+        for (size_t j = pieces.size(); j < (size_t)kTPB; ++j)
+          L.b_seg[bin * kTPB + j] = BinSeg{f, -1, -1, 0};
+      }
+    }
   const int64_t g2 = (n + 1023) / 1024;
   L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
   const int64_t per = (n + L.G2 - 1) / L.G2;
@@ -185,7 +262,7 @@ struct tpl_ctx_s {
 };
 
 namespace {
-enum GraphKind { kGPass1 = 0, kGStandard = 1, kGPass2 = 2 };
+enum GraphKind { kGPass1 = 0, kGStandard = 1, kGPass2 = 2, kGPass2Steps = 3 };
 }
 
 struct tpl_op_s {
@@ -194,17 +271,14 @@ struct tpl_op_s {
   hipStream_t stream = nullptr;
   int64_t n = 0, nnz = 0;
   std::vector<int32_t> h_rowptr;
-  int32_t* d_rowptr = nullptr;
-  int32_t* d_col = nullptr;
-  double* d_val = nullptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
   SchedParams sp;
   Layout lay;
-  int32_t* d_lrows = nullptr;
-  int32_t* d_loff = nullptr;
+  int32_t* d_bcol = nullptr;
+  double* d_bval = nullptr;
+  BinSeg* d_bseg = nullptr;
   double* d_P = nullptr;
-  int32_t* d_cnt = nullptr;
   int32_t* d_srows = nullptr;
   int32_t* d_scol = nullptr;
   double* d_sval = nullptr;
@@ -225,6 +299,10 @@ struct tpl_op_s {
   size_t vcols = 0;
   std::map<std::pair<int, size_t>, hipGraphExec_t> graphs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // live timing (tpl_op_enable_timing): events recorded inside the captured passes
+  bool timing = false;
+  hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
+  int64_t p2_launches = 0;
 };
 
 namespace {
@@ -237,27 +315,24 @@ bool use_graphs() {
 CsrDev csr_dev(const tpl_op_s* op) {
   const Layout& L = op->lay;
   CsrDev A;
-  A.row_ptr = op->d_rowptr;
-  A.col = op->d_col;
-  A.val = op->d_val;
-  A.lrows = op->d_lrows;
-  A.loff = op->d_loff;
-  A.P = op->d_P;
-  A.cnt = op->d_cnt;
   A.srows = op->d_srows;
   A.s_col = op->d_scol;
   A.s_val = op->d_sval;
   A.c_base = op->d_cbase;
   A.c_width = op->d_cwidth;
+  A.b_col = op->d_bcol;
+  A.b_val = op->d_bval;
+  A.b_seg = op->d_bseg;
+  A.P = op->d_P;
   A.s_width = L.s_width;
   A.s_identity = L.s_identity;
   A.n_short = (int32_t)L.srows.size();
   A.n_chunks = (int32_t)L.c_base.size();
   A.n_long = (int32_t)L.lrows.size();
-  A.n_groups = (A.n_long + kLongRowsPerGroup - 1) / kLongRowsPerGroup;
-  A.n_slice_blocks = kSlices * A.n_groups;
+  A.bin_cap = L.bin_cap;
+  A.n_slice_blocks = kSlices * L.M;
   A.G2 = L.G2;
-  A.NA = A.n_chunks + A.n_groups;
+  A.NA = A.n_chunks + A.n_long;
   A.pad = 0;
   A.n = op->n;
   A.E = L.E;
@@ -281,23 +356,18 @@ void upload(T** dst, const std::vector<T>& src) {
 void rebuild_schedule(tpl_op_s* op) {
   op->lay = build_layout(op->n, op->h_rowptr, op->h_col, op->h_val, op->sp);
   const Layout& L = op->lay;
-  upload(&op->d_lrows, L.lrows);
-  upload(&op->d_loff, L.loff);
   upload(&op->d_srows, L.srows);
   upload(&op->d_scol, L.s_col);
   upload(&op->d_sval, L.s_val);
   upload(&op->d_cbase, L.c_base);
   upload(&op->d_cwidth, L.c_width);
-  if (op->d_P) HIPCHK(hipFree(op->d_P));
-  if (op->d_cnt) HIPCHK(hipFree(op->d_cnt));
-  op->d_P = nullptr;
-  op->d_cnt = nullptr;
-  if (!L.lrows.empty()) {
-    const size_t groups = (L.lrows.size() + kLongRowsPerGroup - 1) / kLongRowsPerGroup;
-    HIPCHK(hipMalloc(&op->d_P, L.lrows.size() * kSlices * sizeof(double)));
-    HIPCHK(hipMalloc(&op->d_cnt, groups * sizeof(int32_t)));
-    HIPCHK(hipMemset(op->d_cnt, 0, groups * sizeof(int32_t))); // arrival counters start at 0
-  }
+  upload(&op->d_bcol, L.b_col);
+  upload(&op->d_bval, L.b_val);
+  upload(&op->d_bseg, L.b_seg);
+  // piece slots start empty (sentinel)
+  std::vector<unsigned long long> empty(std::max<size_t>(L.lrows.size() * kSlices, 1),
+                                        kSliceSentinel);
+  upload(reinterpret_cast<unsigned long long**>(&op->d_P), empty);
   drop_graphs(op);
   // partial buffers depend on the layout: force state reallocation
   op->kcap = 0;
@@ -401,14 +471,20 @@ void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
   }
 }
 
-void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
-  const CsrDev A = csr_dev(op);
+void enqueue_pass2_init(tpl_op_s* op, double* Vout) {
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, op->stream));
+}
+void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
+  const CsrDev A = csr_dev(op);
   for (int j = 1; j < (int)steps; ++j) {
     double* Vcol = Vout ? Vout + (size_t)j * op->n : nullptr;
     HIPCHK(launch::p2_spmv(A, op->S, op->V2[j % 3], j >= 2 ? op->V2[(j - 1) % 3] : nullptr,
                            op->V2[(j + 1) % 3], op->x, Vcol, j, op->stream));
   }
+}
+void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
+  enqueue_pass2_init(op, Vout);
+  enqueue_pass2_steps(op, steps, Vout);
 }
 
 template <class Enq>
@@ -439,6 +515,20 @@ void run_graph(tpl_op_s* op, int kind, size_t key, Enq&& enqueue) {
   HIPCHK(hipGraphLaunch(it->second, op->stream));
 }
 
+// Pass two without a basis. With live timing on, the prologue is launched on its own
+// and events bracket the graph of the steps - 1 step launches (tpl_op_pass_timing).
+void run_pass2(tpl_op_s* op, size_t steps) {
+  if (!op->timing) {
+    run_graph(op, kGPass2, steps, [&] { enqueue_pass2(op, steps, nullptr); });
+    return;
+  }
+  enqueue_pass2_init(op, nullptr);
+  HIPCHK(hipEventRecord(op->tev[2], op->stream));
+  run_graph(op, kGPass2Steps, steps, [&] { enqueue_pass2_steps(op, steps, nullptr); });
+  HIPCHK(hipEventRecord(op->tev[3], op->stream));
+  op->p2_launches = (int64_t)steps - 1;
+}
+
 struct HostDecomp {
   int32_t flags[4];
   double b_norm;
@@ -448,13 +538,15 @@ struct HostDecomp {
 };
 
 // Copy flags | norms[0] | alphas | betas back (one D2H), synchronise.
+void sync_checked(tpl_op_s* op) { HIPCHK(hipStreamSynchronize(op->stream)); }
+
 HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
   const size_t kc = op->kcap;
   char* h = (char*)op->h_state;
   const size_t bytes = 16 + ((kc + 1) + 2 * kc) * sizeof(double);
   (void)k;
   HIPCHK(hipMemcpyAsync(h, op->d_state, bytes, hipMemcpyDeviceToHost, op->stream));
-  HIPCHK(hipStreamSynchronize(op->stream));
+  sync_checked(op);
   HostDecomp d;
   std::memcpy(d.flags, h, 16);
   const double* norms = (const double*)(h + 16);
@@ -472,7 +564,9 @@ void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV,
   if (reorth) {
     enqueue_pass1(op, k, true, true); // eager: reorth launch counts vary with j
   } else {
+    if (op->timing) HIPCHK(hipEventRecord(op->tev[0], op->stream));
     run_graph(op, storeV ? kGStandard : kGPass1, k, [&] { enqueue_pass1(op, k, storeV, false); });
+    if (op->timing) HIPCHK(hipEventRecord(op->tev[1], op->stream));
   }
 }
 
@@ -501,7 +595,7 @@ void zero_out(tpl_op_s* op, double* x_out, int mem) {
   if (op->n == 0) return;
   if (mem == TPL_MEM_DEVICE) {
     HIPCHK(hipMemsetAsync(x_out, 0, op->n * sizeof(double), op->stream));
-    HIPCHK(hipStreamSynchronize(op->stream));
+    sync_checked(op);
   } else {
     std::memset(x_out, 0, op->n * sizeof(double));
   }
@@ -584,15 +678,6 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
     for (int64_t i = 0; i <= n; ++i) op->h_rowptr[i] = (int32_t)row_ptr[i];
     op->h_col.assign(col_idx, col_idx + nnz);
     op->h_val.assign(vals, vals + nnz);
-    HIPCHK(hipMalloc(&op->d_rowptr, (n + 1) * sizeof(int32_t)));
-    HIPCHK(hipMemcpy(op->d_rowptr, op->h_rowptr.data(), (n + 1) * sizeof(int32_t),
-                     hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&op->d_col, std::max<int64_t>(nnz, 1) * sizeof(int32_t)));
-    HIPCHK(hipMalloc(&op->d_val, std::max<int64_t>(nnz, 1) * sizeof(double)));
-    if (nnz > 0) {
-      HIPCHK(hipMemcpy(op->d_col, col_idx, nnz * sizeof(int32_t), hipMemcpyHostToDevice));
-      HIPCHK(hipMemcpy(op->d_val, vals, nnz * sizeof(double), hipMemcpyHostToDevice));
-    }
     rebuild_schedule(op.get());
     // vectors: b, R0..2, W, x, V2_0..2, tmp = 10 vectors, each padded to 64 doubles
     op->ld = ((std::max<int64_t>(n, 1) + 63) / 64) * 64;
@@ -610,6 +695,7 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
     op->tmp = p;
     HIPCHK(hipEventCreate(&op->ev0));
     HIPCHK(hipEventCreate(&op->ev1));
+    for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
     *out = op.release();
   });
 }
@@ -620,12 +706,9 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipSetDevice(op->device);
     hipStreamSynchronize(op->stream);
     drop_graphs(op);
-    hipFree(op->d_rowptr);
-    hipFree(op->d_col);
-    hipFree(op->d_val);
-    for (void* p : {(void*)op->d_lrows, (void*)op->d_loff, (void*)op->d_P, (void*)op->d_cnt,
-                    (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval, (void*)op->d_cbase,
-                    (void*)op->d_cwidth})
+    for (void* p : {(void*)op->d_bcol, (void*)op->d_bval, (void*)op->d_bseg, (void*)op->d_P,
+                    (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval,
+                    (void*)op->d_cbase, (void*)op->d_cwidth})
       if (p) hipFree(p);
     hipFree(op->d_vecs);
     if (op->d_state) hipFree(op->d_state);
@@ -634,6 +717,8 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     if (op->d_V) hipFree(op->d_V);
     if (op->ev0) hipEventDestroy(op->ev0);
     if (op->ev1) hipEventDestroy(op->ev1);
+    for (hipEvent_t e : op->tev)
+      if (e) hipEventDestroy(e);
     delete op;
   });
 }
@@ -649,7 +734,7 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
     upload_vec(op, op->tmp, x, mem);
     HIPCHK(launch::spmv(csr_dev(op), op->tmp, op->W, op->stream));
     download_vec(op, y, op->W, op->n, mem);
-    HIPCHK(hipStreamSynchronize(op->stream));
+    sync_checked(op);
   });
 }
 
@@ -714,7 +799,7 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
     *b_norm = d.b_norm;
     if (v_out && d.steps > 0) {
       download_vec(op, v_out, op->d_V, (int64_t)d.steps * op->n, mem);
-      HIPCHK(hipStreamSynchronize(op->stream));
+      sync_checked(op);
     }
   });
 }
@@ -754,11 +839,11 @@ tpl_status tpl_lanczos_pass_two(tpl_op_t op, const double* b, int64_t b_len, con
       ensure_basis(op, steps);
       enqueue_pass2(op, steps, op->d_V);
     } else {
-      run_graph(op, kGPass2, steps, [&] { enqueue_pass2(op, steps, nullptr); });
+      run_pass2(op, steps);
     }
     download_vec(op, x_out, op->x, op->n, mem);
     if (v_out) download_vec(op, v_out, op->d_V, (int64_t)steps * op->n, mem);
-    HIPCHK(hipStreamSynchronize(op->stream));
+    sync_checked(op);
   });
 }
 
@@ -785,9 +870,9 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
     HIPCHK(hipMemcpyAsync(op->S.y, y.data(), d.steps * sizeof(double), hipMemcpyHostToDevice,
                           op->stream));
     // 4. pass two (:174)
-    run_graph(op, kGPass2, d.steps, [&] { enqueue_pass2(op, d.steps, nullptr); });
+    run_pass2(op, d.steps);
     download_vec(op, x_out, op->x, op->n, mem);
-    HIPCHK(hipStreamSynchronize(op->stream));
+    sync_checked(op);
   });
 }
 
@@ -814,7 +899,7 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
     // 3. x = ||b|| V_k y' (:96-104)
     HIPCHK(launch::gemv_recon(op->n, (int)d.steps, op->S, op->d_V, op->x, op->stream));
     download_vec(op, x_out, op->x, op->n, mem);
-    HIPCHK(hipStreamSynchronize(op->stream));
+    sync_checked(op);
   });
 }
 
@@ -836,9 +921,9 @@ tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     set_device(op);
-    if (short_row_max > 0) op->sp.short_row_max = short_row_max;
+    if (short_row_max != 0) op->sp.short_row_max = short_row_max < 0 ? -1 : short_row_max;
     if (max_g2 > 0) op->sp.max_g2 = max_g2;
-    HIPCHK(hipStreamSynchronize(op->stream));
+    sync_checked(op);
     rebuild_schedule(op);
   });
 }
@@ -867,6 +952,31 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
   }
 }
 
+tpl_status tpl_op_enable_timing(tpl_op_t op, int on) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    op->timing = on != 0;
+    op->p2_launches = 0;
+  });
+}
+
+tpl_status tpl_op_pass_timing(tpl_op_t op, double* pass1_us, double* pass2_spmv_us,
+                              int64_t* pass2_launches) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    if (!op->timing || op->p2_launches <= 0)
+      fail(TPL_ERR_INVALID_ARGUMENT, "no timed solve (enable timing, then run a two-pass solve)");
+    set_device(op);
+    HIPCHK(hipEventSynchronize(op->tev[3]));
+    float a = 0.f, b = 0.f;
+    HIPCHK(hipEventElapsedTime(&a, op->tev[0], op->tev[1]));
+    HIPCHK(hipEventElapsedTime(&b, op->tev[2], op->tev[3]));
+    if (pass1_us) *pass1_us = 1000.0 * (double)a;
+    if (pass2_spmv_us) *pass2_spmv_us = 1000.0 * (double)b;
+    if (pass2_launches) *pass2_launches = op->p2_launches;
+  });
+}
+
 tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us,
                               double* algo_bytes) {
   return guarded([&] {
@@ -875,7 +985,10 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     if (op->kcap < 4) ensure_state(op, 4);
     const CsrDev A = csr_dev(op);
     const int big = (int)op->kcap; // j < k: the AXPY kernel does its vector work
-    auto launch_one = [&]() {
+    // Launch i of the timed sequence. The pass-two kernel rotates its three basis
+    // buffers exactly as enqueue_pass2 does (the gathered vector is the previous
+    // launch's output, as in a real sweep); the pass-one kernels re-run step 2.
+    auto launch_one = [&](int i) {
       switch (kernel) {
         case TPL_KERNEL_SPMV: HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream)); break;
         case TPL_KERNEL_PASS1_SPMV:
@@ -885,8 +998,8 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
           HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
-          HIPCHK(launch::p2_spmv(A, op->S, op->V2[2], op->V2[1], op->V2[0], op->x, nullptr, 2,
-                                 op->stream));
+          HIPCHK(launch::p2_spmv(A, op->S, op->V2[(i + 2) % 3], op->V2[(i + 1) % 3],
+                                 op->V2[i % 3], op->x, nullptr, 2, op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }
@@ -895,12 +1008,26 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
     HIPCHK(launch::p1_spmv(A, op->S, op->b, nullptr, op->W, nullptr, 1, op->stream));
     HIPCHK(launch::p1_axpy(A, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
-    HIPCHK(hipStreamSynchronize(op->stream));
-    launch_one(); // warm-up
+    HIPCHK(hipMemcpyAsync(op->V2[1], op->b, op->n * sizeof(double), hipMemcpyDeviceToDevice,
+                          op->stream));
+    HIPCHK(hipMemcpyAsync(op->V2[2], op->R[2], op->n * sizeof(double), hipMemcpyDeviceToDevice,
+                          op->stream));
+    sync_checked(op);
+    // The launches are captured into one graph, as the solver runs them: back-to-back
+    // hipLaunchKernel calls would time the host's submission rate for short kernels.
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIPCHK(hipStreamBeginCapture(op->stream, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < iters; ++i) launch_one(i);
+    HIPCHK(hipStreamEndCapture(op->stream, &g));
+    HIPCHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    hipGraphDestroy(g);
+    HIPCHK(hipGraphLaunch(ge, op->stream)); // warm-up
     HIPCHK(hipEventRecord(op->ev0, op->stream));
-    for (int i = 0; i < iters; ++i) launch_one();
+    HIPCHK(hipGraphLaunch(ge, op->stream));
     HIPCHK(hipEventRecord(op->ev1, op->stream));
     HIPCHK(hipEventSynchronize(op->ev1));
+    hipGraphExecDestroy(ge);
     float ms = 0.f;
     HIPCHK(hipEventElapsedTime(&ms, op->ev0, op->ev1));
     *avg_us = 1000.0 * (double)ms / iters;

@@ -106,6 +106,8 @@ tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_in
 tpl_profile_kernel = _sig("tpl_profile_kernel", c_int, c_void_p, c_int, c_int, PD, PD)
 tpl_kernel_algo_bytes = _sig("tpl_kernel_algo_bytes", c_double, c_void_p, c_int)
 tpl_copy_to_host = _sig("tpl_copy_to_host", c_int, c_void_p, c_void_p, c_size_t)
+tpl_op_enable_timing = _sig("tpl_op_enable_timing", c_int, c_void_p, c_int)
+tpl_op_pass_timing = _sig("tpl_op_pass_timing", c_int, c_void_p, PD, PD, POINTER(c_int64))
 
 # built-in f(T_k) solvers: raw C function pointers usable as tpl_ftk_fn
 FTK_INV_PTR = ctypes.cast(lib.tpl_ftk_inv, c_void_p).value
@@ -126,6 +128,7 @@ EXPORTED = [
     "tpl_lanczos_two_pass", "tpl_lanczos_standard", "tpl_lanczos_pass_one",
     "tpl_lanczos_pass_two", "tpl_load_kkt_system", "tpl_csr_host_free", "tpl_op_schedule",
     "tpl_op_set_schedule", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
+    "tpl_op_enable_timing", "tpl_op_pass_timing",
 ]
 
 

@@ -130,6 +130,17 @@ class HipCsrOp:
         check(_lib.tpl_profile_kernel(self._op, kernel, iters, byref(us), byref(by)))
         return us.value, by.value
 
+    def enable_timing(self, on: bool = True):
+        """Record HIP events inside the captured passes of later solves."""
+        check(_lib.tpl_op_enable_timing(self._op, 1 if on else 0))
+
+    def pass_timing(self):
+        """-> (pass-one span us, pass-two step-launch span us, pass-two launches) of the
+        last timed two-pass solve."""
+        p1, p2, n2 = c_double(), c_double(), c_int64()
+        check(_lib.tpl_op_pass_timing(self._op, byref(p1), byref(p2), byref(n2)))
+        return p1.value, p2.value, n2.value
+
     def algo_bytes(self, kernel: int) -> float:
         return float(_lib.tpl_kernel_algo_bytes(self._op, kernel))
 
