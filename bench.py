@@ -38,7 +38,13 @@ def parse():
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--k", type=int, default=500)
-    p.add_argument("--arcs", type=int, default=500000, choices=[5000, 50000, 500000])
+    p.add_argument("--arcs", type=int, default=0,
+                   help="5000/50000/500000 (netgen fixtures) or 5000000 (synthetic); "
+                        "default 500000 at N=1, 5000000 (row-partitioned) at N>1")
+    p.add_argument("--partition", type=int, default=-1,
+                   help="1: row-partitioned operator even at N=1 (default: N>1)")
+    p.add_argument("--single-ref", type=int, default=1,
+                   help="N>1: also time the same workload on rank 0's GPU alone")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU leg")
     p.add_argument("--cpu-k", type=int, default=500, help="k of the bounded CPU sample")
     p.add_argument("--cpu-reps", type=int, default=2, help="CPU sample repetitions")
@@ -65,29 +71,56 @@ def main():
     from tpl_amd.error import check
     from tpl_amd.utils.data_loader import load_kkt_system, write_qfc_3line
 
-    torch.cuda.set_device(local_rank)
-    dmx = os.path.join(ROOT, "tests", "golden", "kkt", f"netgen-{args.arcs}-3.dmx.xz")
-    qfc = os.path.join("/tmp", f"tpl_bench_{args.arcs}_{os.getpid()}.qfc")
-    write_qfc_3line(qfc, args.arcs)
-    kkt = load_kkt_system(dmx, qfc)
-    os.unlink(qfc)
+    device = int(os.environ.get("TPL_DEVICE", local_rank))  # tests: ranks sharing one GPU
+    torch.cuda.set_device(device)
+    partitioned = (world > 1) if args.partition < 0 else bool(args.partition)
+    arcs = args.arcs or (5000000 if partitioned else 500000)
+    if arcs in (5000, 50000, 500000):
+        dmx = os.path.join(ROOT, "tests", "golden", "kkt", f"netgen-{arcs}-3.dmx.xz")
+        qfc = os.path.join("/tmp", f"tpl_bench_{arcs}_{os.getpid()}.qfc")
+        write_qfc_3line(qfc, arcs)
+        kkt = load_kkt_system(dmx, qfc)
+        os.unlink(qfc)
+        data = (f"netgen {arcs}-arc rho=3 instance regenerated from the reference's netgen "
+                "(tests/golden/kkt), b = A(1/sqrt(n))1, qfc 3-line (D empty)")
+    else:
+        from tpl_amd.utils.data_loader import generate_kkt
+        kkt = generate_kkt(arcs, seed=42)
+        data = (f"synthetic {arcs}-arc rho=3 KKT (tpl_generate_kkt seed 42, "
+                f"{kkt.num_nodes} nodes), b = A(1/sqrt(n))1, D empty")
     a = kkt.a
     n = a.shape[0]
     b = a @ np.full(n, 1.0 / np.sqrt(n))  # src/bin/tradeoff.rs:235-236
 
-    op = tpl_amd.HipCsrOp(a, device=local_rank)
-    b_dev = torch.from_numpy(b).cuda(local_rank)
+    if not partitioned:
+        op = tpl_amd.HipCsrOp(a, device=device)
+        b_loc = b
+    else:
+        # row-partitioned operator: RCCL all-gather of the vector per SpMV over xGMI
+        if dist is None:
+            import torch.distributed as dist
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29533")
+            dist.init_process_group("gloo", rank=0, world_size=1)
+        from tpl_amd.dist import DistContext, DistHipCsrOp
+        dctx = DistContext(rank, world, device=device,
+                           transport=os.environ.get("TPL_DIST_TRANSPORT", "rccl"))
+        op = DistHipCsrOp(a, dctx)
+        b_loc = op.local(b)
+    b_dev = torch.from_numpy(np.ascontiguousarray(b_loc)).cuda(device)
     x_dev = torch.empty_like(b_dev)
     torch.cuda.synchronize()
+    nloc = int(b_dev.shape[0])
 
     def solve():
-        check(_lib.tpl_lanczos_two_pass(op.handle, b_dev.data_ptr(), n, args.k, _lib.FTK_INV_PTR,
-                                        None, x_dev.data_ptr(), _lib.TPL_MEM_DEVICE))
+        check(_lib.tpl_lanczos_two_pass(op.handle, b_dev.data_ptr(), nloc, args.k,
+                                        _lib.FTK_INV_PTR, None, x_dev.data_ptr(),
+                                        _lib.TPL_MEM_DEVICE))
 
     op.enable_timing(True)  # event records inside the captured passes (live timing)
     for _ in range(max(args.warmup, 0)):
         solve()
-    dec = tpl_amd.algorithms.lanczos_pass_one(op, b, args.k)
+    dec = tpl_amd.algorithms.lanczos_pass_one(op, b_loc, args.k)
     steps_taken = dec.steps_taken
 
     def barrier():
@@ -121,13 +154,38 @@ def main():
     # FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 correction applied there)
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_k_p2_spmv.json")
-    if os.path.exists(pmc) and args.arcs == 500000:
+    if os.path.exists(pmc) and arcs == 500000 and not partitioned:
         with open(pmc) as f:
             pj = json.load(f)
         traffic, traffic_src = pj["traffic_bytes_per_launch"], pj["source"]
 
-    iters = args.steps * steps_taken * world
+    # N > 1: the ranks run ONE row-partitioned solve together (strong scaling)
+    iters = args.steps * steps_taken
     value = iters / dt
+    single = None
+    if partitioned and args.single_ref:
+        # the same workload on rank 0's GPU alone, for the speed-up of the partition
+        if rank == 0:
+            op1 = tpl_amd.HipCsrOp(a, device=device)
+            bd = torch.from_numpy(b).cuda(device)
+            xd = torch.empty_like(bd)
+
+            def solve1():
+                check(_lib.tpl_lanczos_two_pass(op1.handle, bd.data_ptr(), n, args.k,
+                                                _lib.FTK_INV_PTR, None, xd.data_ptr(),
+                                                _lib.TPL_MEM_DEVICE))
+            solve1()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                solve1()
+            torch.cuda.synchronize()
+            d1 = time.perf_counter() - t1
+            single = {"value": round(args.steps * steps_taken / d1, 2),
+                      "ms_per_step": round(1000.0 * d1 / args.steps, 4),
+                      "speedup_of_partition": round(d1 / dt, 3)}
+            op1.close()
+        barrier()
     out = {
         "metric": METRIC,
         "value": round(value, 2),
@@ -137,16 +195,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * dt / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "netgen 500k-arc rho=3 instance regenerated from the reference's netgen "
-                "(tests/golden/kkt), b = A(1/sqrt(n))1, qfc 3-line (D empty)",
-        "config": {"workload": f"lanczos_two_pass k={args.k} f=inv, {args.arcs}-arc rho=3 KKT "
-                               f"(n={n}, nnz={a.nnz})",
+        "data": data,
+        "config": {"workload": f"lanczos_two_pass k={args.k} f=inv, {arcs}-arc rho=3 KKT "
+                               f"(n={n}, nnz={a.nnz})"
+                               + ("" if not partitioned else f", rows partitioned over {world} GPUs"),
                    "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
-                   "parallelism": "single" if world == 1 else f"replicas{world}"},
-        "roofline": {"bound": "hbm", "kernel": "k_p2_spmv", "achieved": round(achieved, 1),
+                   "graphs": op.uses_graphs,
+                   "parallelism": "single" if not partitioned
+                   else f"rows{world} (in-place all-gather per SpMV, {dctx.transport})"},
+        "roofline": {"bound": "hbm", "kernel": "k_p2_spmv" + ("" if not partitioned else
+                                                             " (+ all-gather, rank 0)"),
+                     "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algo_bytes_per_launch": by,
@@ -155,7 +217,9 @@ def main():
                      "kernels_us_isolated": iso},
     }
 
-    if rank == 0 and args.cpu_baseline:
+    if single is not None:
+        out["single_gpu_same_workload"] = single
+    if rank == 0 and args.cpu_baseline and world == 1 and not partitioned:
         import oracle  # CPU baseline only (reference-order restatement, single thread)
         from oracle import ftk_ref
         o = oracle.Operator(a)
@@ -175,6 +239,9 @@ def main():
         out["speedup_vs_cpu"] = round(value / (kc / tc), 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    op.close()
+    if partitioned:
+        dctx.close()
     if dist is not None:
         dist.barrier()
         dist.destroy_process_group()

@@ -80,6 +80,9 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz,
 tpl_status tpl_op_destroy(tpl_op_t op);
 int64_t tpl_op_nrows(tpl_op_t op); /* LinOp::nrows / ncols */
 int64_t tpl_op_nnz(tpl_op_t op);
+/* Bit 0: row-partitioned operator; bit 1: passes launched eagerly (no hipGraph —
+ * a host transport, or a transport that refused stream capture). -1 if op is NULL. */
+int tpl_op_flags(tpl_op_t op);
 
 /* y = A x  — LinOp::apply (compatibility path; the solvers below keep the whole
  * recurrence on the device and never call this per step).                     */
@@ -173,6 +176,14 @@ typedef struct tpl_csr_host {
  * assemble A = [[D, E^T],[E, 0]] as CSR. Free with tpl_csr_host_free.          */
 tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_csr_host* out);
 void tpl_csr_host_free(tpl_csr_host* csr);
+/* Synthetic KKT instance for the scale-out config (BASELINE.json configs[4]; the
+ * reference has no generator at that size): num_arcs arcs (u, v), u != v, endpoints
+ * uniform from a splitmix64 stream seeded by `seed`, ordered by (tail, head) like
+ * netgen output, D empty (the 3-line qfc case), assembled exactly as
+ * tpl_load_kkt_system assembles a parsed .dmx. num_nodes for a given m follows
+ * data/qcnd/pargen.c:41-50: floor((1 + sqrt(1 + 8m/0.75)) / 2).              */
+tpl_status tpl_generate_kkt(int64_t num_arcs, int64_t num_nodes, uint64_t seed,
+                            tpl_csr_host* out);
 
 /* ---- introspection / measurement ---------------------------------------- */
 /* SpMV layout of the operator (DESIGN.md "SpMV layout"): rows with at most
@@ -198,6 +209,34 @@ tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g
 tpl_status tpl_op_enable_timing(tpl_op_t op, int on);
 tpl_status tpl_op_pass_timing(tpl_op_t op, double* pass1_us, double* pass2_spmv_us,
                               int64_t* pass2_launches);
+
+/* ---- row-partitioned operator over several GPUs ----------
+ * One process per GPU. Rank r holds the rows [starts[r], starts[r+1]) of A; every
+ * SpMV gathers the full vector with an in-place all-gather (RCCL over xGMI), and
+ * alpha / beta combine the ranks' totals (each rank reduces its own partials in the
+ * single-GPU canonical order; the R totals are all-gathered and reduced in rank
+ * order), so all ranks hold bitwise identical alpha, beta and steps. The solver
+ * entry points above take a partitioned operator unchanged; b, x_out and v_out are
+ * then this rank's block of rows. All ranks must make the same calls in the same
+ * order (collective semantics). Re-orthogonalisation is not supported here.      */
+typedef struct tpl_dist_s* tpl_dist_t;
+enum { TPL_DIST_ID_BYTES = 128 };
+/* Contiguous row blocks balanced by algorithmic bytes (12 per nonzero + 40 per row);
+ * host only. starts: nranks + 1 entries.                                           */
+tpl_status tpl_dist_partition(int64_t n, const int64_t* row_ptr, int nranks, int64_t* starts);
+/* RCCL unique id (rank 0 creates it; the caller broadcasts the bytes).            */
+tpl_status tpl_dist_unique_id(uint8_t* id);
+tpl_status tpl_dist_create(int device, int rank, int nranks, const uint8_t* id, tpl_dist_t* out);
+/* Test transport: all-gathers go through a host callback (recv = the ranks' send
+ * buffers concatenated in rank order); synchronous, no graphs.                     */
+typedef int (*tpl_allgather_fn)(const void* send, void* recv, size_t bytes_per_rank, void* user);
+tpl_status tpl_dist_create_host(int device, int rank, int nranks, tpl_allgather_fn fn, void* user,
+                                tpl_dist_t* out);
+tpl_status tpl_dist_destroy(tpl_dist_t d);
+/* This rank's block: row_ptr (n_local + 1, 0-based), global column indices.       */
+tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t* starts,
+                                  const int64_t* row_ptr, const int32_t* col_idx,
+                                  const double* vals, tpl_op_t* out);
 
 /* Kernel ids for tpl_profile_kernel */
 enum {

@@ -1,0 +1,44 @@
+"""One rank of a partitioned GPU solve, started as a child process by
+tests/test_gpu_dist.py (RANK / WORLD_SIZE / MASTER_* in the environment; all ranks
+may share one GPU with the host transport). Writes rank<r>.npz into argv[1]."""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "two-pass-lanczos_amd"))
+
+import numpy as np  # noqa: E402
+
+
+def main():
+    out, transport, arcs, k = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    import torch
+    import torch.distributed as tdist
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    import tpl_amd
+    from tpl_amd.dist import DistContext, DistHipCsrOp
+    from conftest import harness_b, load_kkt
+    a = load_kkt(arcs, out).a
+    b = harness_b(a)
+    ctx = DistContext(rank, world, device=int(os.environ.get("TPL_DEVICE", "0")), transport=transport)
+    op = DistHipCsrOp(a, ctx)
+    bl = op.local(b)
+    x1 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
+    x2 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
+    dec = tpl_amd.algorithms.lanczos_pass_one(op, bl, k)
+    xs = tpl_amd.lanczos(op, bl, k, "inv")
+    y = op.apply(op.local(np.cos(np.arange(a.shape[0]))))
+    np.savez(os.path.join(out, f"rank{rank}.npz"), x1=x1, x2=x2, xs=xs, y=y,
+             al=dec.alphas, be=dec.betas, steps=dec.steps_taken, bn=dec.b_norm,
+             r0=op.row0, r1=op.row1)
+    torch.cuda.synchronize()
+    tdist.barrier()
+    op.close()
+    ctx.close()
+    tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

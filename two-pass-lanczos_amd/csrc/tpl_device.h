@@ -93,6 +93,8 @@ struct CsrDev {
   int32_t n_slice_blocks;   // kSlices * M; SpMV grid = n_chunks + n_slice_blocks
   int32_t G2;               // workgroups of the element-wise kernels == #norm partials
   int32_t NA;               // #alpha partials = n_chunks + n_long
+  int32_t NA_r;             // #alpha partials the reducing kernel reads (NA, or #ranks)
+  int32_t G2_r;             // #norm partials the reducing kernel reads (G2, or #ranks)
   int32_t pad;
   int64_t n;
   int64_t E;                // elements per workgroup of the element-wise kernels
@@ -105,8 +107,13 @@ struct DevState {
   double* alphas;   // alphas[j-1] = alpha_j                              (kcap)
   double* betas;    // betas[j-1]  = beta_j                               (kcap)
   double* y;        // pass-two coefficients y_k (already * ||b||), or y' (kcap)
-  double* Pa;       // alpha partials (NA)
+  double* Pa;       // alpha partials (NA) — written by this rank's kernels
   double* Pb;       // ||.||^2 partials (G2)
+  // What the reducing kernels read: Pa / Pb on one GPU; with the rows partitioned
+  // over R ranks, the R per-rank totals (each = partials() of that rank's Pa / Pb),
+  // all-gathered in rank order.
+  const double* Pa_r;
+  const double* Pb_r;
 };
 
 } // namespace tpl

@@ -504,9 +504,12 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
   if (threadIdx.x == 0) S.Pb[blockIdx.x] = p;
 }
 
-// Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1).
+// Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1), this rank's rows;
+// xsrc = the gather source holding r_j for every column (== r_cur on one GPU, the
+// all-gathered vector when the rows are partitioned over ranks).
 template <int CW>
 __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, DevState S,
+                                                  const double* __restrict__ xsrc,
                                                   const double* __restrict__ r_cur,
                                                   const double* __restrict__ r_prev,
                                                   double* __restrict__ W,
@@ -515,7 +518,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   extern __shared__ double lds[];
   const int stop = S.flags[0]; // checked after the loads are in flight
   PartialRegs<4> pr;           // G2 <= 1024
-  load_partials(S.Pb, A.G2, pr);
+  load_partials(S.Pb_r, A.G2_r, pr);
   const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
   EpiPass1 epi;
   epi.r_cur = r_cur;
@@ -530,7 +533,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   // beta_{j-1} (||b|| at j = 1) from the norm partials; fills the epilogue.
   auto scale_fn = [&]() -> Scale {
     if (stop) return Scale{0.0, false};
-    const double beta = sqrt(finish_partials(S.Pb, A.G2, pr, red));
+    const double beta = sqrt(finish_partials(S.Pb_r, A.G2_r, pr, red));
     if (beta <= kBreakdownTol) {
       // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
       // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed
@@ -550,7 +553,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
     return Scale{epi.invN_cur, true};
   };
   double acc = 0.0;
-  const int slot = spmv_block<CW>(A, r_cur, scale_fn, epi, acc, lds);
+  const int slot = spmv_block<CW>(A, xsrc, scale_fn, epi, acc, lds);
   if (slot < 0) return; // uniform per workgroup
   const double p = block_sum(acc, red);
   if (threadIdx.x == 0) S.Pa[slot] = p;
@@ -564,7 +567,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   __shared__ double red[4];
   const int stop = S.flags[0];
   PartialRegs<12> pr;
-  load_partials(S.Pa, A.NA, pr);
+  load_partials(S.Pa_r, A.NA_r, pr);
   const int64_t beg = (int64_t)blockIdx.x * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
   const double normj = S.norms[j - 1];
@@ -576,7 +579,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     rc0 = *reinterpret_cast<const double2*>(r_cur + i00);
   }
   if (stop) return;
-  const double alpha = finish_partials(S.Pa, A.NA, pr, red);
+  const double alpha = finish_partials(S.Pa_r, A.NA_r, pr, red);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
@@ -630,6 +633,7 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
 // Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x.
 template <int CW>
 __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, DevState S,
+                                                  const double* __restrict__ xsrc,
                                                   const double* __restrict__ v_cur,
                                                   const double* __restrict__ v_prev,
                                                   double* __restrict__ v_next,
@@ -648,7 +652,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, 
   epi.x = x;
   epi.Vcol = Vcol;
   double acc = 0.0;
-  spmv_block<CW>(A, v_cur, UnitScale{}, epi, acc, lds);
+  spmv_block<CW>(A, xsrc, UnitScale{}, epi, acc, lds);
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
@@ -779,9 +783,9 @@ hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStrea
   hipLaunchKernelGGL(k_p1_init, dim3(A.G2), dim3(kTPB), 0, s, A, S, b);
   return hipGetLastError();
 }
-hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
-                   double* W, double* Vcol, int j, hipStream_t s) {
-  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, r_cur, r_prev, W, Vcol, j);
+hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
+                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
+  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
@@ -794,9 +798,11 @@ hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, do
   hipLaunchKernelGGL(k_p2_init, dim3(elem_grid(n)), dim3(kTPB), 0, s, n, S, b, v1, x, Vcol);
   return hipGetLastError();
 }
-hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
-                   double* v_next, double* x, double* Vcol, int j, hipStream_t s) {
-  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, v_cur, v_prev, v_next, x, Vcol, j);
+hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
+                   const double* v_prev, double* v_next, double* x, double* Vcol, int j,
+                   hipStream_t s) {
+  if (spmv_grid(A) > 0)
+    TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,

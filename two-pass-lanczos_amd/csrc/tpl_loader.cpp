@@ -15,6 +15,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <cstring>
 #include <fstream>
 #include <string>
@@ -130,76 +131,12 @@ struct Trip {
   double v;
 };
 
-} // namespace
-
-extern "C" {
-
-tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_csr_host* out) {
-  try {
-    if (!dmx_path || !qfc_path || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
-    std::memset(out, 0, sizeof(*out));
-    // ---- parse_dmx (:68-156)
-    std::FILE* fd = std::fopen(dmx_path, "rb");
-    if (!fd) err_io(errno);
-    FileGuard gd{fd};
-    std::setvbuf(fd, nullptr, _IOFBF, 1 << 20);
-    size_t num_nodes = 0, num_arcs = 0, arc_counter = 0;
-    bool found = false;
-    std::vector<int64_t> eu, ev; // per arc: row of +1, row of -1
-    std::string line;
-    while (next_line(fd, line)) {
-      const std::vector<std::string> parts = split_ws(line);
-      if (parts.empty()) continue;
-      const std::string& t = parts[0];
-      if (t == "c") continue;
-      if (t == "p") {
-        if (parts.size() >= 4 && parts[1] == "min") {
-          if (!parse_usize(parts[2], num_nodes)) err_parse_int(parts[2]);
-          if (!parse_usize(parts[3], num_arcs)) err_parse_int(parts[3]);
-          found = true;
-        } else {
-          err_problem_line();
-        }
-      } else if (t == "a") {
-        // (the reference indexes parts[1], parts[2] unchecked and would panic)
-        const std::string su = parts.size() > 1 ? parts[1] : std::string();
-        const std::string sv = parts.size() > 2 ? parts[2] : std::string();
-        size_t u, v;
-        if (!parse_usize(su, u)) err_parse_int(su);
-        if (u == 0) err_node_index(su);
-        if (!parse_usize(sv, v)) err_parse_int(sv);
-        if (v == 0) err_node_index(sv);
-        eu.push_back((int64_t)u - 1);
-        ev.push_back((int64_t)v - 1);
-        ++arc_counter;
-      }
-    }
-    if (std::ferror(fd)) err_io(EIO);
-    if (!found) err_problem_line();
-    // SparseColMat::try_new_from_triplets(num_nodes, num_arcs, ...) bounds check (:152-153)
-    for (size_t j = 0; j < arc_counter; ++j)
-      if (j >= num_arcs || (size_t)eu[j] >= num_nodes || (size_t)ev[j] >= num_nodes)
-        err_construction();
-
-    // ---- parse_qfc (:166-198)
-    std::FILE* fq = std::fopen(qfc_path, "rb");
-    if (!fq) err_io(errno);
-    FileGuard gq{fq};
-    if (!next_line(fq, line)) err_eof();
-    size_t m_from_file;
-    if (!parse_usize(line, m_from_file)) err_parse_int("m");
-    if (m_from_file != num_arcs) err_arc_mismatch(m_from_file, num_arcs);
-    for (size_t s = 0; s < num_arcs; ++s)
-      if (!next_line(fq, line)) break;
-    std::vector<double> qcost;
-    for (size_t s = 0; s < num_arcs; ++s) {
-      if (!next_line(fq, line)) break;
-      double c;
-      if (!parse_f64(line, c)) err_parse_float(line);
-      qcost.push_back(c);
-    }
-
-    // ---- load_kkt_system (:211-259): CSR of [[D, E^T], [E, 0]]
+// CSR of A = [[D, E^T], [E, 0]] (load_kkt_system, src/utils/data_loader.rs:211-259):
+// arc j has tail eu[j] (+1) and head ev[j] (-1); arcs j >= arc_counter are absent;
+// qcost holds the D diagonal entries present (the 3-line qfc yields none).
+void assemble_kkt(size_t num_nodes, size_t num_arcs, size_t arc_counter,
+                  const std::vector<int64_t>& eu, const std::vector<int64_t>& ev,
+                  const std::vector<double>& qcost, tpl_csr_host* out) {
     const int64_t m = (int64_t)num_arcs, p = (int64_t)num_nodes, n = m + p;
     if (n >= INT32_MAX) fail(TPL_ERR_UNSUPPORTED, "n must be < 2^31");
     // E column j holds rows eu[j] (+1) and ev[j] (-1), summed if equal (faer sums duplicates).
@@ -274,6 +211,119 @@ tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_c
       std::memcpy(out->col_idx, col.data(), nnz * sizeof(int32_t));
       std::memcpy(out->vals, val.data(), nnz * sizeof(double));
     }
+}
+
+} // namespace
+
+extern "C" {
+
+tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_csr_host* out) {
+  try {
+    if (!dmx_path || !qfc_path || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    std::memset(out, 0, sizeof(*out));
+    // ---- parse_dmx (:68-156)
+    std::FILE* fd = std::fopen(dmx_path, "rb");
+    if (!fd) err_io(errno);
+    FileGuard gd{fd};
+    std::setvbuf(fd, nullptr, _IOFBF, 1 << 20);
+    size_t num_nodes = 0, num_arcs = 0, arc_counter = 0;
+    bool found = false;
+    std::vector<int64_t> eu, ev; // per arc: row of +1, row of -1
+    std::string line;
+    while (next_line(fd, line)) {
+      const std::vector<std::string> parts = split_ws(line);
+      if (parts.empty()) continue;
+      const std::string& t = parts[0];
+      if (t == "c") continue;
+      if (t == "p") {
+        if (parts.size() >= 4 && parts[1] == "min") {
+          if (!parse_usize(parts[2], num_nodes)) err_parse_int(parts[2]);
+          if (!parse_usize(parts[3], num_arcs)) err_parse_int(parts[3]);
+          found = true;
+        } else {
+          err_problem_line();
+        }
+      } else if (t == "a") {
+        // (the reference indexes parts[1], parts[2] unchecked and would panic)
+        const std::string su = parts.size() > 1 ? parts[1] : std::string();
+        const std::string sv = parts.size() > 2 ? parts[2] : std::string();
+        size_t u, v;
+        if (!parse_usize(su, u)) err_parse_int(su);
+        if (u == 0) err_node_index(su);
+        if (!parse_usize(sv, v)) err_parse_int(sv);
+        if (v == 0) err_node_index(sv);
+        eu.push_back((int64_t)u - 1);
+        ev.push_back((int64_t)v - 1);
+        ++arc_counter;
+      }
+    }
+    if (std::ferror(fd)) err_io(EIO);
+    if (!found) err_problem_line();
+    // SparseColMat::try_new_from_triplets(num_nodes, num_arcs, ...) bounds check (:152-153)
+    for (size_t j = 0; j < arc_counter; ++j)
+      if (j >= num_arcs || (size_t)eu[j] >= num_nodes || (size_t)ev[j] >= num_nodes)
+        err_construction();
+
+    // ---- parse_qfc (:166-198)
+    std::FILE* fq = std::fopen(qfc_path, "rb");
+    if (!fq) err_io(errno);
+    FileGuard gq{fq};
+    if (!next_line(fq, line)) err_eof();
+    size_t m_from_file;
+    if (!parse_usize(line, m_from_file)) err_parse_int("m");
+    if (m_from_file != num_arcs) err_arc_mismatch(m_from_file, num_arcs);
+    for (size_t s = 0; s < num_arcs; ++s)
+      if (!next_line(fq, line)) break;
+    std::vector<double> qcost;
+    for (size_t s = 0; s < num_arcs; ++s) {
+      if (!next_line(fq, line)) break;
+      double c;
+      if (!parse_f64(line, c)) err_parse_float(line);
+      qcost.push_back(c);
+    }
+
+    assemble_kkt(num_nodes, num_arcs, arc_counter, eu, ev, qcost, out);
+    tpl::set_last_error("");
+    return TPL_OK;
+  } catch (const tpl::Error& e) {
+    tpl::set_last_error(e.msg);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    tpl::set_last_error("host allocation failed");
+    return TPL_ERR_OUT_OF_MEMORY;
+  }
+}
+
+tpl_status tpl_generate_kkt(int64_t num_arcs, int64_t num_nodes, uint64_t seed,
+                            tpl_csr_host* out) {
+  try {
+    if (!out) fail(TPL_ERR_INVALID_ARGUMENT, "out is NULL");
+    *out = tpl_csr_host{};
+    if (num_arcs < 1 || num_nodes < 2) fail(TPL_ERR_INVALID_ARGUMENT, "need >= 1 arc and >= 2 nodes");
+    // Arcs (u, v), u != v, endpoints uniform (splitmix64 stream), then ordered by tail
+    // node and head like netgen's output (each node's outgoing arcs contiguous).
+    uint64_t st = seed;
+    auto next = [&st]() {
+      uint64_t z = (st += 0x9E3779B97F4A7C15ULL);
+      z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+      z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+      return z ^ (z >> 31);
+    };
+    const uint64_t p = (uint64_t)num_nodes;
+    std::vector<std::pair<int64_t, int64_t>> arcs((size_t)num_arcs);
+    for (auto& a : arcs) {
+      const int64_t u = (int64_t)(next() % p);
+      int64_t v = (int64_t)(next() % (p - 1));
+      if (v >= u) ++v;
+      a = {u, v};
+    }
+    std::sort(arcs.begin(), arcs.end());
+    std::vector<int64_t> eu((size_t)num_arcs), ev((size_t)num_arcs);
+    for (size_t j = 0; j < arcs.size(); ++j) {
+      eu[j] = arcs[j].first;
+      ev[j] = arcs[j].second;
+    }
+    assemble_kkt((size_t)num_nodes, (size_t)num_arcs, (size_t)num_arcs, eu, ev, {}, out);
     tpl::set_last_error("");
     return TPL_OK;
   } catch (const tpl::Error& e) {

@@ -9,6 +9,7 @@
 // host round trip of a solve is the f(T_k) call between the passes, exactly
 // where the reference calls its closure (src/solvers.rs:71-75, :155-156).
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cmath>
@@ -28,14 +29,15 @@ namespace tpl {
 namespace launch {
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s);
-hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* r_cur, const double* r_prev,
-                   double* W, double* Vcol, int j, hipStream_t s);
+hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
+                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, hipStream_t s);
-hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* v_cur, const double* v_prev,
-                   double* v_next, double* x, double* Vcol, int j, hipStream_t s);
+hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
+                   const double* v_prev, double* v_next, double* x, double* Vcol, int j,
+                   hipStream_t s);
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
                       hipStream_t s);
 hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
@@ -136,9 +138,26 @@ static int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, in
   return std::max<int32_t>(4, std::min<int32_t>(kShortRowMax, 2 * median));
 }
 
-static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
+// Column index as stored on the device: the identity on one GPU; with the rows
+// partitioned over ranks, global column c (owned by rank r, rows [starts[r],
+// starts[r+1])) lives at r * ld + (c - starts[r]) of the all-gathered vector.
+struct ColMap {
+  const std::vector<int64_t>* starts = nullptr;  // nullptr: identity
+  int64_t ld = 0;
+  int32_t operator()(int32_t c) const {
+    if (!starts) return c;
+    const auto it = std::upper_bound(starts->begin(), starts->end(), (int64_t)c);
+    const int64_t r = (it - starts->begin()) - 1;
+    return (int32_t)(r * ld + (c - (*starts)[r]));
+  }
+};
+
+// n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds
+// are taken on global column indices, so a partition of one rank reproduces the
+// single-GPU layout exactly).
+static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
                            const std::vector<int32_t>& col, const std::vector<double>& val,
-                           const SchedParams& sp) {
+                           const SchedParams& sp, const ColMap& cmap) {
   Layout L;
   const int32_t T = short_row_threshold(n, rp, sp.short_row_max);
   for (int64_t i = 0; i < n; ++i) {
@@ -172,7 +191,7 @@ static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
       const int32_t r = L.srows[p];
       for (int32_t k = 0; k < rp[r + 1] - rp[r]; ++k) {
         const int64_t e = L.c_base[c] + (int64_t)k * kChunkRows + (p - c * kChunkRows);
-        L.s_col[e] = col[rp[r] + k];
+        L.s_col[e] = cmap(col[rp[r] + k]);
         L.s_val[e] = val[rp[r] + k];
       }
     }
@@ -191,7 +210,7 @@ static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
     const int32_t row = L.lrows[r];
     int32_t q = rp[row];
     for (int s = 0; s <= kSlices; ++s) {
-      const int64_t bound = n * s / kSlices;
+      const int64_t bound = n_glob * s / kSlices;
       while (q < rp[row + 1] && col[q] < bound) ++q;
       poff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
       if (s > 0)
@@ -235,7 +254,7 @@ static Layout build_layout(int64_t n, const std::vector<int32_t>& rp,
           const int32_t q0 = poff[r * (kSlices + 1) + s], q1 = poff[r * (kSlices + 1) + s + 1];
           L.b_seg[bin * kTPB + j] = BinSeg{start, r, L.lrows[r], 0};
           for (int32_t q = q0; q < q1; ++q) {
-            L.b_col[bin * L.bin_cap + start + (q - q0)] = col[q];
+            L.b_col[bin * L.bin_cap + start + (q - q0)] = cmap(col[q]);
             L.b_val[bin * L.bin_cap + start + (q - q0)] = val[q];
           }
         }
@@ -261,6 +280,16 @@ struct tpl_ctx_s {
   hipStream_t stream = nullptr;
 };
 
+// A rank of a row-partitioned operator (tpl_dist_create*): its GPU and stream, and the
+// transport of the per-step exchanges — RCCL over xGMI, or (tests) a host callback.
+struct tpl_dist_s {
+  tpl_ctx_s ctx;
+  int rank = 0, nranks = 1;
+  ncclComm_t comm = nullptr;
+  tpl_allgather_fn host_fn = nullptr;
+  void* host_user = nullptr;
+};
+
 namespace {
 enum GraphKind { kGPass1 = 0, kGStandard = 1, kGPass2 = 2, kGPass2Steps = 3 };
 }
@@ -269,7 +298,12 @@ struct tpl_op_s {
   tpl_ctx_s* ctx = nullptr;
   int device = 0;
   hipStream_t stream = nullptr;
-  int64_t n = 0, nnz = 0;
+  int64_t n = 0, nnz = 0;           // this operator's rows (the rank's block) and nonzeros
+  // row partition (tpl_dist_op_create_csr); single GPU: dist == nullptr, n_glob == n
+  tpl_dist_s* dist = nullptr;
+  int64_t n_glob = 0;
+  std::vector<int64_t> starts;
+  bool eager = false;               // launch without graphs (host transport / no capture)
   std::vector<int32_t> h_rowptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
@@ -289,6 +323,11 @@ struct tpl_op_s {
   int64_t ld = 0;
   double *b = nullptr, *R[3] = {nullptr, nullptr, nullptr}, *W = nullptr, *x = nullptr,
          *V2[3] = {nullptr, nullptr, nullptr}, *tmp = nullptr;
+  // gather sources of the SpMV: the same buffers on one GPU; with a partition, the
+  // all-gathered vectors (nranks x ld) whose rank-th slice the local pointers view
+  double *bG = nullptr, *RG[3] = {nullptr, nullptr, nullptr}, *V2G[3] = {nullptr, nullptr, nullptr},
+         *tmpG = nullptr;
+  double* d_rsum = nullptr;         // [nranks alpha totals][nranks norm totals] (partition)
   // solver state
   size_t kcap = 0;
   void* d_state = nullptr;  // flags | norms | alphas | betas | y | Pa | Pb | Pr
@@ -333,6 +372,8 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.n_slice_blocks = kSlices * L.M;
   A.G2 = L.G2;
   A.NA = A.n_chunks + A.n_long;
+  A.NA_r = op->dist ? op->dist->nranks : A.NA;
+  A.G2_r = op->dist ? op->dist->nranks : A.G2;
   A.pad = 0;
   A.n = op->n;
   A.E = L.E;
@@ -354,7 +395,12 @@ void upload(T** dst, const std::vector<T>& src) {
 }
 
 void rebuild_schedule(tpl_op_s* op) {
-  op->lay = build_layout(op->n, op->h_rowptr, op->h_col, op->h_val, op->sp);
+  ColMap cmap;
+  if (op->dist) {
+    cmap.starts = &op->starts;
+    cmap.ld = op->ld;
+  }
+  op->lay = build_layout(op->n, op->n_glob, op->h_rowptr, op->h_col, op->h_val, op->sp, cmap);
   const Layout& L = op->lay;
   upload(&op->d_srows, L.srows);
   upload(&op->d_scol, L.s_col);
@@ -398,6 +444,8 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->S.y = op->S.betas + kc;
     op->S.Pa = op->S.y + kc;
     op->S.Pb = op->S.Pa + std::max(A.NA, 1);
+    op->S.Pa_r = op->dist ? op->d_rsum : op->S.Pa;
+    op->S.Pb_r = op->dist ? op->d_rsum + op->dist->nranks : op->S.Pb;
     op->kcap = kc;
   }
   if (reorth && !op->d_Pr) {
@@ -437,12 +485,50 @@ void download_vec(tpl_op_s* op, double* dst, const double* src, int64_t count, i
                         op->stream));
 }
 
-// r_j buffer of pass one: r_1 = b, then R[j % 3].
-inline const double* r_of(const tpl_op_s* op, int j) { return j == 1 ? op->b : op->R[j % 3]; }
+// r_j buffer of pass one: r_1 = b, then R[j % 3] (local view, and gather source).
+inline double* r_of(const tpl_op_s* op, int j) { return j == 1 ? op->b : op->R[j % 3]; }
+inline double* rG_of(const tpl_op_s* op, int j) { return j == 1 ? op->bG : op->RG[j % 3]; }
+
+// ---- exchanges of a row-partitioned operator -------------------------------------
+#define NCCLCHK(expr)                                                                       \
+  do {                                                                                      \
+    ncclResult_t r_ = (expr);                                                               \
+    if (r_ != ncclSuccess)                                                                  \
+      ::tpl::fail(TPL_ERR_DEVICE, std::string(#expr) + ": " + ncclGetErrorString(r_));     \
+  } while (0)
+
+// In-place all-gather of `count` doubles per rank: rank r's part sits at base + r*count.
+void dist_allgather(tpl_op_s* op, double* base, size_t count) {
+  tpl_dist_s* d = op->dist;
+  if (d->comm) {
+    NCCLCHK(ncclAllGather(base + (size_t)d->rank * count, base, count, ncclDouble, d->comm,
+                          op->stream));
+    return;
+  }
+  // host transport (tests): stage through host memory around the callback
+  std::vector<double> send(count), recv(count * (size_t)d->nranks);
+  HIPCHK(hipMemcpyAsync(send.data(), base + (size_t)d->rank * count, count * sizeof(double),
+                        hipMemcpyDeviceToHost, op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+  if (d->host_fn(send.data(), recv.data(), count * sizeof(double), d->host_user) != 0)
+    fail(TPL_ERR_DEVICE, "host all-gather callback failed");
+  HIPCHK(hipMemcpyAsync(base, recv.data(), recv.size() * sizeof(double), hipMemcpyHostToDevice,
+                        op->stream));
+  HIPCHK(hipStreamSynchronize(op->stream));
+}
+void dist_group(tpl_op_s* op, bool begin) {
+  if (op->dist && op->dist->comm) NCCLCHK(begin ? ncclGroupStart() : ncclGroupEnd());
+}
+// This rank's total of a partial array, in the single-GPU canonical order, into
+// its slot of the all-gathered totals.
+void dist_total(tpl_op_s* op, const double* P, int N, double* slot) {
+  HIPCHK(launch::reorth_reduce(1, P, N, slot, op->stream));
+}
 
 // ---- reorthogonalisation (extension, not in the reference): classical Gram-Schmidt,
 // applied twice, of r_{j+1} against the stored columns V[:, 0..j) before beta_j.
 void enqueue_reorth(tpl_op_s* op, int j) {
+  if (op->dist) fail(TPL_ERR_UNSUPPORTED, "re-orthogonalisation of a partitioned operator");
   const int cols = j; // v_1 .. v_j are stored in V[:, 0..j)
   const int G2 = op->lay.G2;
   const int64_t E = op->lay.E;
@@ -458,28 +544,62 @@ void enqueue_reorth(tpl_op_s* op, int j) {
   }
 }
 
-void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
+// Pass one prologue: ||b||^2 partials; with a partition, b and the per-rank
+// totals are all-gathered (step 1 gathers from b).
+void enqueue_p1_prologue(tpl_op_s* op) {
   const CsrDev A = csr_dev(op);
   HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
+  if (op->dist) {
+    const int R = op->dist->nranks;
+    dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
+    dist_group(op, true);
+    dist_allgather(op, op->d_rsum + R, 1);
+    dist_allgather(op, op->bG, (size_t)op->ld);
+    dist_group(op, false);
+  }
+}
+
+// Pass one, step j (k = requested steps).
+void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
+  const CsrDev A = csr_dev(op);
+  HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
+                         op->W, Vcol, j, op->stream));
+  if (op->dist) {
+    dist_total(op, op->S.Pa, A.NA, op->d_rsum + op->dist->rank);
+    dist_allgather(op, op->d_rsum, 1);
+  }
+  HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
+  if (op->dist && j < k) {
+    const int R = op->dist->nranks;
+    dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
+    dist_group(op, true);
+    dist_allgather(op, op->d_rsum + R, 1);
+    dist_allgather(op, op->RG[(j + 1) % 3], (size_t)op->ld);
+    dist_group(op, false);
+  }
+}
+
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
+  enqueue_p1_prologue(op);
   for (int j = 1; j <= (int)k; ++j) {
     double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
-    HIPCHK(launch::p1_spmv(A, op->S, r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr, op->W,
-                           Vcol, j, op->stream));
-    HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, (int)k,
-                           op->stream));
+    enqueue_p1_step(op, j, (int)k, Vcol);
     if (reorth && j < (int)k) enqueue_reorth(op, j);
   }
 }
 
 void enqueue_pass2_init(tpl_op_s* op, double* Vout) {
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, op->stream));
+  if (op->dist) dist_allgather(op, op->V2G[1], (size_t)op->ld);
 }
 void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
   const CsrDev A = csr_dev(op);
   for (int j = 1; j < (int)steps; ++j) {
     double* Vcol = Vout ? Vout + (size_t)j * op->n : nullptr;
-    HIPCHK(launch::p2_spmv(A, op->S, op->V2[j % 3], j >= 2 ? op->V2[(j - 1) % 3] : nullptr,
-                           op->V2[(j + 1) % 3], op->x, Vcol, j, op->stream));
+    HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
+                           j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
+                           Vcol, j, op->stream));
+    if (op->dist && j + 1 < (int)steps) dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
   }
 }
 void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
@@ -489,7 +609,7 @@ void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
 
 template <class Enq>
 void run_graph(tpl_op_s* op, int kind, size_t key, Enq&& enqueue) {
-  if (!use_graphs()) {
+  if (!use_graphs() || op->eager) {
     enqueue();
     return;
   }
@@ -502,13 +622,23 @@ void run_graph(tpl_op_s* op, int kind, size_t key, Enq&& enqueue) {
       hipGraph_t g = nullptr;
       hipStreamEndCapture(op->stream, &g);
       if (g) hipGraphDestroy(g);
-      throw;
+      if (!op->dist) throw;
+      op->eager = true;  // the transport refused capture: launch eagerly from now on
+      hipGetLastError();
+      enqueue();
+      return;
     }
     hipGraph_t g = nullptr;
-    HIPCHK(hipStreamEndCapture(op->stream, &g));
+    hipError_t e = hipStreamEndCapture(op->stream, &g);
     hipGraphExec_t ge = nullptr;
-    hipError_t e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
+    if (e == hipSuccess) e = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (g) hipGraphDestroy(g);
+    if (e != hipSuccess && op->dist) {
+      op->eager = true;
+      hipGetLastError();
+      enqueue();
+      return;
+    }
     HIPCHK(e);
     it = op->graphs.emplace(std::make_pair(kind, key), ge).first;
   }
@@ -601,6 +731,43 @@ void zero_out(tpl_op_s* op, double* x_out, int mem) {
   }
 }
 
+// Layout, vectors and events of a freshly filled operator (single GPU or one rank
+// of a partition; the vector stride ld is common to all ranks).
+void init_op(tpl_op_s* op) {
+  const int R = op->dist ? op->dist->nranks : 1;
+  int64_t widest = op->n;
+  if (op->dist)
+    for (int r = 0; r < R; ++r) widest = std::max(widest, op->starts[r + 1] - op->starts[r]);
+  op->ld = ((std::max<int64_t>(widest, 1) + 63) / 64) * 64;
+  rebuild_schedule(op);
+  // gathered: b, R0..2, V2_0..2, tmp (R x ld each); local: W, x (ld each)
+  const size_t gathered = 8 * (size_t)R * op->ld, local = 2 * (size_t)op->ld;
+  HIPCHK(hipMalloc(&op->d_vecs, (gathered + local) * sizeof(double)));
+  HIPCHK(hipMemset(op->d_vecs, 0, (gathered + local) * sizeof(double)));
+  double* p = op->d_vecs;
+  const size_t gl = (size_t)R * op->ld, own = (size_t)(op->dist ? op->dist->rank : 0) * op->ld;
+  op->bG = p;
+  p += gl;
+  for (int i = 0; i < 3; ++i, p += gl) op->RG[i] = p;
+  for (int i = 0; i < 3; ++i, p += gl) op->V2G[i] = p;
+  op->tmpG = p;
+  p += gl;
+  op->W = p;
+  p += op->ld;
+  op->x = p;
+  op->b = op->bG + own;
+  for (int i = 0; i < 3; ++i) op->R[i] = op->RG[i] + own;
+  for (int i = 0; i < 3; ++i) op->V2[i] = op->V2G[i] + own;
+  op->tmp = op->tmpG + own;
+  if (op->dist) {
+    HIPCHK(hipMalloc(&op->d_rsum, 2 * (size_t)R * sizeof(double)));
+    HIPCHK(hipMemset(op->d_rsum, 0, 2 * (size_t)R * sizeof(double)));
+  }
+  HIPCHK(hipEventCreate(&op->ev0));
+  HIPCHK(hipEventCreate(&op->ev1));
+  for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
+}
+
 } // namespace
 
 // =========================================================== C ABI
@@ -673,29 +840,13 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
     op->device = ctx->device;
     op->stream = ctx->stream;
     op->n = n;
+    op->n_glob = n;
     op->nnz = nnz;
     op->h_rowptr.resize(n + 1);
     for (int64_t i = 0; i <= n; ++i) op->h_rowptr[i] = (int32_t)row_ptr[i];
     op->h_col.assign(col_idx, col_idx + nnz);
     op->h_val.assign(vals, vals + nnz);
-    rebuild_schedule(op.get());
-    // vectors: b, R0..2, W, x, V2_0..2, tmp = 10 vectors, each padded to 64 doubles
-    op->ld = ((std::max<int64_t>(n, 1) + 63) / 64) * 64;
-    HIPCHK(hipMalloc(&op->d_vecs, 10 * op->ld * sizeof(double)));
-    HIPCHK(hipMemset(op->d_vecs, 0, 10 * op->ld * sizeof(double)));
-    double* p = op->d_vecs;
-    op->b = p;
-    p += op->ld;
-    for (int i = 0; i < 3; ++i, p += op->ld) op->R[i] = p;
-    op->W = p;
-    p += op->ld;
-    op->x = p;
-    p += op->ld;
-    for (int i = 0; i < 3; ++i, p += op->ld) op->V2[i] = p;
-    op->tmp = p;
-    HIPCHK(hipEventCreate(&op->ev0));
-    HIPCHK(hipEventCreate(&op->ev1));
-    for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
+    init_op(op.get());
     *out = op.release();
   });
 }
@@ -711,6 +862,7 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
                     (void*)op->d_cbase, (void*)op->d_cwidth})
       if (p) hipFree(p);
     hipFree(op->d_vecs);
+    if (op->d_rsum) hipFree(op->d_rsum);
     if (op->d_state) hipFree(op->d_state);
     if (op->h_state) hipHostFree(op->h_state);
     if (op->d_Pr) hipFree(op->d_Pr);
@@ -724,6 +876,10 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
 }
 
 int64_t tpl_op_nrows(tpl_op_t op) { return op ? op->n : -1; }
+int tpl_op_flags(tpl_op_t op) {
+  if (!op) return -1;
+  return (op->dist ? 1 : 0) | (op->eager ? 2 : 0);
+}
 int64_t tpl_op_nnz(tpl_op_t op) { return op ? op->nnz : -1; }
 
 tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
@@ -732,7 +888,8 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
     set_device(op);
     if (op->n == 0) return;
     upload_vec(op, op->tmp, x, mem);
-    HIPCHK(launch::spmv(csr_dev(op), op->tmp, op->W, op->stream));
+    if (op->dist) dist_allgather(op, op->tmpG, (size_t)op->ld);
+    HIPCHK(launch::spmv(csr_dev(op), op->tmpG, op->W, op->stream));
     download_vec(op, y, op->W, op->n, mem);
     sync_checked(op);
   });
@@ -776,13 +933,9 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
       ensure_state(op, k, reorth != 0);
       ensure_basis(op, k);
       upload_vec(op, op->b, b, mem);
-      const CsrDev A = csr_dev(op);
-      HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
+      enqueue_p1_prologue(op);
       for (int j = 1; j <= (int)k; ++j) {
-        HIPCHK(launch::p1_spmv(A, op->S, r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr, op->W,
-                               op->d_V + (size_t)(j - 1) * op->n, j, op->stream));
-        HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, (int)k,
-                               op->stream));
+        enqueue_p1_step(op, j, (int)k, op->d_V + (size_t)(j - 1) * op->n);
         d = fetch_decomp(op, k);
         if (d.flags[0] || d.steps < (size_t)j) break; // zero b or breakdown before step j
         const int go = cb((size_t)j, op->d_V, op->n, d.alphas, d.steps, d.betas,
@@ -992,13 +1145,14 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
       switch (kernel) {
         case TPL_KERNEL_SPMV: HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream)); break;
         case TPL_KERNEL_PASS1_SPMV:
-          HIPCHK(launch::p1_spmv(A, op->S, op->R[2], op->b, op->W, nullptr, 2, op->stream));
+          HIPCHK(launch::p1_spmv(A, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
+                                 op->stream));
           break;
         case TPL_KERNEL_PASS1_AXPY:
           HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
-          HIPCHK(launch::p2_spmv(A, op->S, op->V2[(i + 2) % 3], op->V2[(i + 1) % 3],
+          HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3], op->V2[(i + 1) % 3],
                                  op->V2[i % 3], op->x, nullptr, 2, op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
@@ -1006,7 +1160,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     };
     // Valid state for repeated launches: flags clear, partials/norms of a real step.
     HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
-    HIPCHK(launch::p1_spmv(A, op->S, op->b, nullptr, op->W, nullptr, 1, op->stream));
+    HIPCHK(launch::p1_spmv(A, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
     HIPCHK(launch::p1_axpy(A, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[1], op->b, op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));
@@ -1032,6 +1186,130 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     HIPCHK(hipEventElapsedTime(&ms, op->ev0, op->ev1));
     *avg_us = 1000.0 * (double)ms / iters;
     if (algo_bytes) *algo_bytes = tpl_kernel_algo_bytes(op, kernel);
+  });
+}
+
+
+// ------------------------------------------------------------ row partition
+tpl_status tpl_dist_partition(int64_t n, const int64_t* row_ptr, int nranks, int64_t* starts) {
+  return guarded([&] {
+    if (!row_ptr || !starts || nranks < 1) fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
+    if (n < nranks) fail(TPL_ERR_INVALID_ARGUMENT, "fewer rows than ranks");
+    // Contiguous row blocks balanced by algorithmic bytes: 12 per nonzero (value +
+    // column) + 40 per row (pass two's vector traffic), cut where the prefix crosses
+    // r/nranks of the total; every block keeps at least one row.
+    auto cost = [&](int64_t i) { return 12.0 * (double)row_ptr[i] + 40.0 * (double)i; };
+    const double total = cost(n);
+    starts[0] = 0;
+    int64_t i = 0;
+    for (int r = 1; r < nranks; ++r) {
+      const double target = total * r / nranks;
+      while (i < n && cost(i) < target) ++i;
+      starts[r] = std::min<int64_t>(std::max<int64_t>(i, starts[r - 1] + 1), n - (nranks - r));
+      i = starts[r];
+    }
+    starts[nranks] = n;
+  });
+}
+
+tpl_status tpl_dist_unique_id(uint8_t* id) {
+  return guarded([&] {
+    if (!id) fail(TPL_ERR_INVALID_ARGUMENT, "id is NULL");
+    static_assert(sizeof(ncclUniqueId) == TPL_DIST_ID_BYTES, "ncclUniqueId size");
+    ncclUniqueId u;
+    NCCLCHK(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof(u));
+  });
+}
+
+static tpl_dist_s* new_dist(int device, int rank, int nranks) {
+  int cnt = 0;
+  if (hipGetDeviceCount(&cnt) != hipSuccess || cnt == 0) fail(TPL_ERR_DEVICE, "no HIP device available");
+  if (device < 0 || device >= cnt) fail(TPL_ERR_INVALID_ARGUMENT, "device index out of range");
+  if (nranks < 1 || rank < 0 || rank >= nranks) fail(TPL_ERR_INVALID_ARGUMENT, "bad rank / nranks");
+  HIPCHK(hipSetDevice(device));
+  auto d = std::make_unique<tpl_dist_s>();
+  d->ctx.device = device;
+  d->rank = rank;
+  d->nranks = nranks;
+  HIPCHK(hipStreamCreateWithFlags(&d->ctx.stream, hipStreamNonBlocking));
+  return d.release();
+}
+
+tpl_status tpl_dist_create(int device, int rank, int nranks, const uint8_t* id, tpl_dist_t* out) {
+  return guarded([&] {
+    if (!id || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    std::unique_ptr<tpl_dist_s> d(new_dist(device, rank, nranks));
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof(u));
+    NCCLCHK(ncclCommInitRank(&d->comm, nranks, u, rank));
+    *out = d.release();
+  });
+}
+
+tpl_status tpl_dist_create_host(int device, int rank, int nranks, tpl_allgather_fn fn, void* user,
+                                tpl_dist_t* out) {
+  return guarded([&] {
+    if (!fn || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    std::unique_ptr<tpl_dist_s> d(new_dist(device, rank, nranks));
+    d->host_fn = fn;
+    d->host_user = user;
+    *out = d.release();
+  });
+}
+
+tpl_status tpl_dist_destroy(tpl_dist_t d) {
+  return guarded([&] {
+    if (!d) return;
+    hipSetDevice(d->ctx.device);
+    if (d->ctx.stream) hipStreamSynchronize(d->ctx.stream);
+    if (d->comm) ncclCommDestroy(d->comm);
+    if (d->ctx.stream) hipStreamDestroy(d->ctx.stream);
+    delete d;
+  });
+}
+
+tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t* starts,
+                                  const int64_t* row_ptr, const int32_t* col_idx,
+                                  const double* vals, tpl_op_t* out) {
+  return guarded([&] {
+    if (!d || !starts || !row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    const int R = d->nranks;
+    if (starts[0] != 0 || starts[R] != n_global) fail(TPL_ERR_INVALID_ARGUMENT, "bad partition");
+    for (int r = 0; r < R; ++r)
+      if (starts[r + 1] <= starts[r]) fail(TPL_ERR_INVALID_ARGUMENT, "empty or unordered block");
+    if (n_global >= INT32_MAX / 2) fail(TPL_ERR_UNSUPPORTED, "n must be < 2^30");
+    const int64_t n = starts[d->rank + 1] - starts[d->rank];
+    const int64_t nnz = row_ptr[n];
+    if (row_ptr[0] != 0 || nnz < 0 || nnz >= INT32_MAX)
+      fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0; nnz < 2^31");
+    if (nnz > 0 && (!col_idx || !vals)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    for (int64_t i = 0; i < n; ++i) {
+      if (row_ptr[i + 1] < row_ptr[i]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
+      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+        const int32_t c = col_idx[q];
+        if (c < 0 || c >= n_global) fail(TPL_ERR_INVALID_ARGUMENT, "column index out of range");
+        if (q > row_ptr[i] && c <= col_idx[q - 1])
+          fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be strictly ascending per row");
+      }
+    }
+    HIPCHK(hipSetDevice(d->ctx.device));
+    auto op = std::make_unique<tpl_op_s>();
+    op->ctx = &d->ctx;
+    op->device = d->ctx.device;
+    op->stream = d->ctx.stream;
+    op->dist = d;
+    op->eager = d->comm == nullptr;
+    op->n = n;
+    op->n_glob = n_global;
+    op->nnz = nnz;
+    op->starts.assign(starts, starts + R + 1);
+    op->h_rowptr.resize(n + 1);
+    for (int64_t i = 0; i <= n; ++i) op->h_rowptr[i] = (int32_t)row_ptr[i];
+    op->h_col.assign(col_idx, col_idx + nnz);
+    op->h_val.assign(vals, vals + nnz);
+    init_op(op.get());
+    *out = op.release();
   });
 }
 

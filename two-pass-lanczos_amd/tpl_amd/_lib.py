@@ -85,6 +85,7 @@ tpl_op_create_csr = _sig("tpl_op_create_csr", c_int, c_void_p, c_int64, c_int64,
 tpl_op_destroy = _sig("tpl_op_destroy", c_int, c_void_p)
 tpl_op_nrows = _sig("tpl_op_nrows", c_int64, c_void_p)
 tpl_op_nnz = _sig("tpl_op_nnz", c_int64, c_void_p)
+tpl_op_flags = _sig("tpl_op_flags", c_int, c_void_p)
 tpl_op_apply = _sig("tpl_op_apply", c_int, c_void_p, c_void_p, c_void_p, c_int)
 tpl_lanczos = _sig("tpl_lanczos", c_int, c_void_p, c_void_p, c_int64, c_size_t, c_void_p,
                    c_void_p, c_void_p, c_int)
@@ -100,6 +101,8 @@ tpl_lanczos_pass_two = _sig("tpl_lanczos_pass_two", c_int, c_void_p, c_void_p, c
                             c_void_p, c_int)
 tpl_load_kkt_system = _sig("tpl_load_kkt_system", c_int, c_char_p, c_char_p, POINTER(CsrHost))
 tpl_csr_host_free = _sig("tpl_csr_host_free", None, POINTER(CsrHost))
+tpl_generate_kkt = _sig("tpl_generate_kkt", c_int, c_int64, c_int64, ctypes.c_uint64,
+                        POINTER(CsrHost))
 tpl_op_schedule = _sig("tpl_op_schedule", c_int, c_void_p, POINTER(c_int32), POINTER(c_int32),
                        POINTER(c_int32), POINTER(c_int64), POINTER(c_int32), POINTER(c_int32))
 tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_int32)
@@ -128,10 +131,26 @@ EXPORTED = [
     "tpl_lanczos_two_pass", "tpl_lanczos_standard", "tpl_lanczos_pass_one",
     "tpl_lanczos_pass_two", "tpl_load_kkt_system", "tpl_csr_host_free", "tpl_op_schedule",
     "tpl_op_set_schedule", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
-    "tpl_op_enable_timing", "tpl_op_pass_timing",
+    "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_generate_kkt", "tpl_op_flags",
 ]
 
 
 def last_error() -> str:
     m = tpl_last_error()
     return m.decode("utf-8", "replace") if m else ""
+
+# row-partitioned operator (include/tpl.h, "row-partitioned operator over several GPUs")
+TPL_DIST_ID_BYTES = 128
+ALLGATHER_FN = CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
+tpl_dist_partition = _sig("tpl_dist_partition", c_int, c_int64, POINTER(c_int64), c_int,
+                          POINTER(c_int64))
+tpl_dist_unique_id = _sig("tpl_dist_unique_id", c_int, POINTER(ctypes.c_uint8))
+tpl_dist_create = _sig("tpl_dist_create", c_int, c_int, c_int, c_int, POINTER(ctypes.c_uint8),
+                       POINTER(c_void_p))
+tpl_dist_create_host = _sig("tpl_dist_create_host", c_int, c_int, c_int, c_int, ALLGATHER_FN,
+                            c_void_p, POINTER(c_void_p))
+tpl_dist_destroy = _sig("tpl_dist_destroy", c_int, c_void_p)
+tpl_dist_op_create_csr = _sig("tpl_dist_op_create_csr", c_int, c_void_p, c_int64, POINTER(c_int64),
+                              POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p))
+EXPORTED += ["tpl_dist_partition", "tpl_dist_unique_id", "tpl_dist_create",
+             "tpl_dist_create_host", "tpl_dist_destroy", "tpl_dist_op_create_csr"]

@@ -1,0 +1,116 @@
+"""Row-partitioned operator over several GPUs (include/tpl.h).
+
+One process per GPU. Rank r owns the rows [starts[r], starts[r+1]) of A (contiguous
+blocks balanced by algorithmic bytes, ``partition``); each SpMV all-gathers the
+vector in place over RCCL/xGMI and alpha/beta combine the ranks' totals in rank
+order, so every rank holds the same alpha, beta and steps bit for bit. The solver
+entry points (``tpl_amd.lanczos_two_pass``, ``algorithms.*``) take a ``DistHipCsrOp``
+unchanged; ``b`` and the returned ``x`` are then this rank's block of rows.
+
+Transports: ``"rccl"`` (the product path; the RCCL unique id is broadcast with
+torch.distributed) and ``"host"`` (tests: all-gathers through torch.distributed on
+host memory, eager launches) — e.g. several ranks sharing one GPU.
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import POINTER, byref, c_double, c_int32, c_int64, c_void_p
+
+import numpy as np
+
+from . import _lib
+from .error import check
+from .operator import HipCsrOp, _as_csr_arrays
+
+
+def partition(a, nranks: int) -> np.ndarray:
+    """starts[nranks + 1] of the byte-balanced contiguous row blocks (tpl_dist_partition)."""
+    n, rp, _, _ = _as_csr_arrays(a)
+    starts = np.zeros(nranks + 1, dtype=np.int64)
+    check(_lib.tpl_dist_partition(n, rp.ctypes.data_as(POINTER(c_int64)), nranks,
+                                  starts.ctypes.data_as(POINTER(c_int64))))
+    return starts
+
+
+class DistContext:
+    """This process's rank of a partitioned solve (tpl_dist_create / _create_host)."""
+
+    def __init__(self, rank: int, world: int, device: int = 0, transport: str = "rccl",
+                 group=None):
+        import torch.distributed as tdist
+        self.rank, self.world, self.device, self.transport = rank, world, device, transport
+        h = c_void_p()
+        if transport == "rccl":
+            idb = (ctypes.c_uint8 * _lib.TPL_DIST_ID_BYTES)()
+            if rank == 0:
+                check(_lib.tpl_dist_unique_id(idb))
+            obj = [bytes(idb) if rank == 0 else None]
+            tdist.broadcast_object_list(obj, src=0, group=group)
+            ctypes.memmove(idb, obj[0], _lib.TPL_DIST_ID_BYTES)
+            check(_lib.tpl_dist_create(device, rank, world, idb, byref(h)))
+        elif transport == "host":
+            import torch
+
+            def allgather(send, recv, nbytes, _user):
+                try:
+                    src = torch.frombuffer(bytearray(ctypes.string_at(send, nbytes)),
+                                           dtype=torch.uint8)
+                    parts = [torch.empty(nbytes, dtype=torch.uint8) for _ in range(world)]
+                    tdist.all_gather(parts, src.clone(), group=group)
+                    out = torch.cat(parts).numpy()
+                    ctypes.memmove(recv, out.ctypes.data, nbytes * world)
+                    return 0
+                except Exception:  # pragma: no cover - reported as a device error
+                    return 1
+
+            self._cb = _lib.ALLGATHER_FN(allgather)  # keep alive
+            check(_lib.tpl_dist_create_host(device, rank, world, self._cb, None, byref(h)))
+        else:
+            raise ValueError(f"unknown transport {transport!r}")
+        self._d = h.value
+
+    @property
+    def handle(self) -> int:
+        return self._d
+
+    def close(self):
+        if getattr(self, "_d", None):
+            _lib.tpl_dist_destroy(self._d)
+            self._d = None
+
+    def __del__(self):  # pragma: no cover
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DistHipCsrOp(HipCsrOp):
+    """This rank's block of rows of a symmetric A, resident in its GPU's HBM."""
+
+    def __init__(self, a, ctx: DistContext, starts=None):
+        n, rp, ci, v = _as_csr_arrays(a)
+        self.starts = (partition((n, rp, ci, v), ctx.world) if starts is None
+                       else np.ascontiguousarray(starts, dtype=np.int64))
+        r0, r1 = int(self.starts[ctx.rank]), int(self.starts[ctx.rank + 1])
+        lrp = np.ascontiguousarray(rp[r0:r1 + 1] - rp[r0], dtype=np.int64)
+        lci = np.ascontiguousarray(ci[rp[r0]:rp[r1]], dtype=np.int32)
+        lv = np.ascontiguousarray(v[rp[r0]:rp[r1]], dtype=np.float64)
+        self.device = ctx.device
+        self.dist = ctx
+        self.row0, self.row1, self.n_global = r0, r1, n
+        h = c_void_p()
+        check(_lib.tpl_dist_op_create_csr(
+            ctx.handle, n, self.starts.ctypes.data_as(POINTER(c_int64)),
+            lrp.ctypes.data_as(POINTER(c_int64)), lci.ctypes.data_as(POINTER(c_int32)),
+            lv.ctypes.data_as(POINTER(c_double)), byref(h)))
+        self._op = h.value
+        self._n = r1 - r0
+        self._nnz = int(lrp[-1])
+
+    def ncols(self) -> int:
+        return self.n_global
+
+    def local(self, v):
+        """This rank's block of a global vector."""
+        return v[self.row0:self.row1]

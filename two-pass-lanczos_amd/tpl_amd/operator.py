@@ -93,6 +93,11 @@ class HipCsrOp:
     def handle(self) -> int:
         return self._op
 
+    @property
+    def uses_graphs(self) -> bool:
+        """False when the passes are launched eagerly (see tpl_op_flags)."""
+        return not (int(_lib.tpl_op_flags(self._op)) & 2)
+
     def apply(self, x):
         """y = A x (LinOp::apply)."""
         if _is_torch_cuda(x):

@@ -42,21 +42,39 @@ def _plain(path: str, tmpdir: str) -> str:
     return str(path)
 
 
+def _take(h) -> KKTSystem:
+    try:
+        n, nnz = h.n, h.nnz
+        rp = np.ctypeslib.as_array(h.row_ptr, (n + 1,)).copy()
+        ci = np.ctypeslib.as_array(h.col_idx, (max(nnz, 1),))[:nnz].copy()
+        v = np.ctypeslib.as_array(h.vals, (max(nnz, 1),))[:nnz].copy()
+        a = sp.csr_matrix((v, ci, rp), shape=(n, n))
+        return KKTSystem(a=a, num_nodes=int(h.num_nodes), num_arcs=int(h.num_arcs))
+    finally:
+        _lib.tpl_csr_host_free(byref(h))
+
+
 def load_kkt_system(dmx_path, qfc_path) -> KKTSystem:
     with tempfile.TemporaryDirectory(prefix="tpl_kkt_") as td:
         dmx = _plain(dmx_path, td)
         qfc = _plain(qfc_path, td)
         h = _lib.CsrHost()
         check(_lib.tpl_load_kkt_system(dmx.encode(), qfc.encode(), byref(h)))
-        try:
-            n, nnz = h.n, h.nnz
-            rp = np.ctypeslib.as_array(h.row_ptr, (n + 1,)).copy()
-            ci = np.ctypeslib.as_array(h.col_idx, (max(nnz, 1),))[:nnz].copy()
-            v = np.ctypeslib.as_array(h.vals, (max(nnz, 1),))[:nnz].copy()
-            a = sp.csr_matrix((v, ci, rp), shape=(n, n))
-            return KKTSystem(a=a, num_nodes=int(h.num_nodes), num_arcs=int(h.num_arcs))
-        finally:
-            _lib.tpl_csr_host_free(byref(h))
+        return _take(h)
+
+
+def pargen_nodes(num_arcs: int) -> int:
+    """Node count of a rho = 3 instance with m arcs (data/qcnd/pargen.c:41-50)."""
+    return int(np.floor((1.0 + np.sqrt(1.0 + 8.0 * num_arcs / 0.75)) / 2.0))
+
+
+def generate_kkt(num_arcs: int, num_nodes: int | None = None, seed: int = 42) -> KKTSystem:
+    """Synthetic KKT instance (BASELINE.json configs[4], 5M arcs): uniform arcs u != v
+    ordered by (tail, head), D empty, assembled like load_kkt_system (tpl_generate_kkt)."""
+    p = pargen_nodes(num_arcs) if num_nodes is None else int(num_nodes)
+    h = _lib.CsrHost()
+    check(_lib.tpl_generate_kkt(int(num_arcs), p, int(seed), byref(h)))
+    return _take(h)
 
 
 def write_qfc_3line(path: str, m: int, seed: int = 0) -> None:
