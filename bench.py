@@ -205,9 +205,11 @@ def main():
                    "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
                    "graphs": op.uses_graphs,
                    "parallelism": "single" if not partitioned
-                   else f"rows{world} (in-place all-gather per SpMV, {dctx.transport})"},
+                   else (f"{op.mode}{world} (" + ("long-row partials all-gathered per SpMV"
+                         if op.mode == "replicated" else "vector all-gathered per SpMV")
+                         + f", {dctx.transport})")},
         "roofline": {"bound": "hbm", "kernel": "k_p2_spmv" + ("" if not partitioned else
-                                                             " (+ all-gather, rank 0)"),
+                                                             " (+ exchange, rank 0)"),
                      "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,

@@ -233,10 +233,24 @@ typedef int (*tpl_allgather_fn)(const void* send, void* recv, size_t bytes_per_r
 tpl_status tpl_dist_create_host(int device, int rank, int nranks, tpl_allgather_fn fn, void* user,
                                 tpl_dist_t* out);
 tpl_status tpl_dist_destroy(tpl_dist_t d);
-/* This rank's block: row_ptr (n_local + 1, 0-based), global column indices.       */
+/* This rank's block: row_ptr (n_local + 1, 0-based), global column indices.
+ * Every SpMV all-gathers the whole vector (8n bytes moved per SpMV).              */
 tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t* starts,
                                   const int64_t* row_ptr, const int32_t* col_idx,
                                   const double* vals, tpl_op_t* out);
+/* Replicated-long-row partition (the structure-aware split of SURVEY.md §8(e)), from
+ * the WHOLE matrix (every rank passes the same CSR): the short rows are split into
+ * contiguous byte-balanced blocks; the long rows are replicated — each rank sums the
+ * entries in the columns it owns, the n_long partials are all-gathered (8 n_long
+ * bytes per rank per SpMV) and every rank finishes them in rank order. Needs no halo:
+ * a short row may only reference its own block and the long rows (true for the KKT
+ * matrices: arc rows reference node rows only), else TPL_ERR_UNSUPPORTED.
+ * This rank's vector is [its short rows | all long rows] (tpl_op_local_rows).        */
+tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t* row_ptr,
+                                         const int32_t* col_idx, const double* vals,
+                                         tpl_op_t* out);
+/* Global row index of each entry of this operator's vectors (tpl_op_nrows entries). */
+tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows);
 
 /* Kernel ids for tpl_profile_kernel */
 enum {

@@ -13,6 +13,7 @@ import numpy as np  # noqa: E402
 
 def main():
     out, transport, arcs, k = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
+    mode = sys.argv[5] if len(sys.argv) > 5 else "auto"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     import torch
     import torch.distributed as tdist
@@ -23,7 +24,7 @@ def main():
     a = load_kkt(arcs, out).a
     b = harness_b(a)
     ctx = DistContext(rank, world, device=int(os.environ.get("TPL_DEVICE", "0")), transport=transport)
-    op = DistHipCsrOp(a, ctx)
+    op = DistHipCsrOp(a, ctx, mode=mode)
     bl = op.local(b)
     x1 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
     x2 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
@@ -32,7 +33,7 @@ def main():
     y = op.apply(op.local(np.cos(np.arange(a.shape[0]))))
     np.savez(os.path.join(out, f"rank{rank}.npz"), x1=x1, x2=x2, xs=xs, y=y,
              al=dec.alphas, be=dec.betas, steps=dec.steps_taken, bn=dec.b_norm,
-             r0=op.row0, r1=op.row1)
+             rows=op.local_rows, mode=op.mode)
     torch.cuda.synchronize()
     tdist.barrier()
     op.close()

@@ -1,10 +1,11 @@
 """GPU tests of the row-partitioned operator.
 
-* one rank over RCCL: the partitioned path reproduces the single-GPU result bit
-  for bit (same layout, the rank total of alpha/beta partials is exact);
+* one rank over RCCL, row blocks: the partitioned path reproduces the single-GPU
+  result bit for bit (same layout, the rank total of alpha/beta partials is exact);
+  replicated long rows: within 1e-10;
 * two and three ranks sharing this box's GPU, exchanging through the host transport
-  (RCCL refuses two ranks on one device): identical coefficients on every rank,
-  deterministic, x within 1e-10 of the single-GPU solve, exact SpMV blocks.
+  (RCCL refuses two ranks on one device), both partitions: identical coefficients on
+  every rank, deterministic, x within 1e-10 of the single-GPU solve, SpMV blocks.
 The ranks run as child processes (tests/dist_worker.py)."""
 import os
 import socket
@@ -29,14 +30,14 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(tmp, world, transport, arcs=5000, k=50):
+def _run_ranks(tmp, world, transport, mode="auto", arcs=5000, k=50):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
-                                       tmp, transport, str(arcs), str(k)], env=env))
+                                       tmp, transport, str(arcs), str(k), mode], env=env))
     rcs = [p.wait(timeout=300) for p in procs]
     assert rcs == [0] * world, rcs
     return [np.load(os.path.join(tmp, f"rank{r}.npz")) for r in range(world)]
@@ -51,29 +52,53 @@ def _single(kkt_tmp, arcs=5000, k=50):
             tpl_amd.algorithms.lanczos_pass_one(op, b, k), tpl_amd.lanczos(op, b, k, "inv"))
 
 
-def test_one_rank_rccl_bitwise(kkt_tmp, tmp_path):
+def _assemble(rs, key, n):
+    out = np.full(n, np.nan)
+    for r in rs:
+        out[r["rows"]] = r[key]
+    return out
+
+
+def test_one_rank_rccl_rows_bitwise(kkt_tmp, tmp_path):
     a, x, dec, xs = _single(kkt_tmp)
-    r = _run_ranks(str(tmp_path), 1, "rccl")[0]
+    r = _run_ranks(str(tmp_path), 1, "rccl", mode="rows")[0]
+    assert str(r["mode"]) == "rows"
     assert np.array_equal(r["x1"], x)
     assert np.array_equal(r["al"], dec.alphas) and np.array_equal(r["be"], dec.betas)
     assert np.array_equal(r["xs"], xs)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_ranks_share_gpu_host_transport(kkt_tmp, tmp_path, world):
+def test_one_rank_rccl_replicated(kkt_tmp, tmp_path):
     a, x, dec, xs = _single(kkt_tmp)
-    rs = _run_ranks(str(tmp_path), world, "host")
+    r = _run_ranks(str(tmp_path), 1, "rccl", mode="replicated")[0]
+    assert str(r["mode"]) == "replicated"
+    xr = _assemble([r], "x1", a.shape[0])
+    assert np.linalg.norm(xr - x) <= 1e-10 * np.linalg.norm(x)
+
+
+@pytest.mark.parametrize("world,mode", [(2, "rows"), (3, "rows"), (2, "replicated"),
+                                        (3, "replicated")])
+def test_ranks_share_gpu_host_transport(kkt_tmp, tmp_path, world, mode):
+    a, x, dec, xs = _single(kkt_tmp)
+    rs = _run_ranks(str(tmp_path), world, "host", mode=mode)
+    assert all(str(r["mode"]) == mode for r in rs)
     for r in rs[1:]:  # every rank holds the same coefficients, bit for bit
         assert np.array_equal(r["al"], rs[0]["al"]) and np.array_equal(r["be"], rs[0]["be"])
     assert int(rs[0]["steps"]) == dec.steps_taken
     np.testing.assert_allclose(rs[0]["al"], dec.alphas, rtol=0, atol=1e-12)
     np.testing.assert_allclose(rs[0]["be"], dec.betas, rtol=1e-12)
-    xd = np.concatenate([r["x1"] for r in rs])
-    assert np.array_equal(xd, np.concatenate([r["x2"] for r in rs]))  # deterministic
+    n = a.shape[0]
+    xd = _assemble(rs, "x1", n)
+    assert np.array_equal(xd, _assemble(rs, "x2", n))  # deterministic
     assert np.linalg.norm(xd - x) <= 1e-10 * np.linalg.norm(x)
-    xsd = np.concatenate([r["xs"] for r in rs])
+    xsd = _assemble(rs, "xs", n)
     assert np.linalg.norm(xsd - xs) <= 1e-10 * np.linalg.norm(xs)
-    # SpMV blocks: +-1 values, exact products; row sums in the same order
-    y = np.concatenate([r["y"] for r in rs])
+    if mode == "replicated":  # the replicated (long) rows hold identical bits on every rank
+        for r in rs[1:]:
+            common, i0, i1 = np.intersect1d(rs[0]["rows"], r["rows"], return_indices=True)
+            assert len(common) > 0
+            assert np.array_equal(rs[0]["x1"][i0], r["x1"][i1])
+    # SpMV blocks: +-1 values, exact products
+    y = _assemble(rs, "y", n)
     yr = a @ np.cos(np.arange(a.shape[0]))
     np.testing.assert_allclose(y, yr, rtol=1e-13, atol=1e-12)

@@ -58,6 +58,7 @@ constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB tab
 #define TPL_BIN_MIN 2048
 #endif
 constexpr int kBinMin = TPL_BIN_MIN; // default entries per bin (8 per thread)
+constexpr int kLongEpiRows = 1024;   // long rows per workgroup of k_long_epi_* (partitioned)
 constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
 // Slice partial slots hold this signalling-NaN bit pattern while empty (arithmetic
 // never produces a signalling NaN, so a published partial can never equal it).
@@ -93,11 +94,18 @@ struct CsrDev {
   int32_t n_slice_blocks;   // kSlices * M; SpMV grid = n_chunks + n_slice_blocks
   int32_t G2;               // workgroups of the element-wise kernels == #norm partials
   int32_t NA;               // #alpha partials = n_chunks + n_long
-  int32_t NA_r;             // #alpha partials the reducing kernel reads (NA, or #ranks)
+  int32_t NA_r;             // #alpha partials the reducing kernel reads (NA, or more, see DevState)
   int32_t G2_r;             // #norm partials the reducing kernel reads (G2, or #ranks)
   int32_t pad;
   int64_t n;
   int64_t E;                // elements per workgroup of the element-wise kernels
+  // Replicated-long-row partition (tpl_runtime.cpp, "hybrid"): the SpMV stores each
+  // long row's rank-local partial in ypart[ri] instead of finishing the row, and the
+  // norm partials cover elements [0, norm_n) only (replicated entries count once).
+  double* ypart;            // n_long partials of this rank (own slice of the all-gather)
+  int32_t long_defer;       // 1: long rows deferred to k_long_epi_*
+  int32_t pad2;
+  int64_t norm_n;           // == n except on ranks that do not own the replicated rows
 };
 
 // Device-resident solver state (one per operator).

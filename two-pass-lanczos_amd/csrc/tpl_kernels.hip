@@ -426,6 +426,10 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   double y = 0.0;
 #pragma unroll
   for (int k = 0; k < kSlices; ++k) y = y + __longlong_as_double((long long)v[k]);
+  if (A.long_defer) {  // partitioned: this rank's part of the row; finished after the exchange
+    A.ypart[sg.ri] = y;
+    return;
+  }
   double acc = 0.0;
   epi.apply(sg.row, y, pre, acc);
   epi.long_alpha(sg.ri, acc);
@@ -493,11 +497,11 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
   for (int64_t i0 = beg + 2 * threadIdx.x; i0 < end; i0 += 2 * kTPB) {
     if (i0 + 1 < end) {
       const double2 v = *reinterpret_cast<const double2*>(b + i0);
-      acc = fma(v.x, v.x, acc);
-      acc = fma(v.y, v.y, acc);
+      acc = i0 < A.norm_n ? fma(v.x, v.x, acc) : acc;
+      acc = i0 + 1 < A.norm_n ? fma(v.y, v.y, acc) : acc;
     } else {
       const double v = b[i0];
-      acc = fma(v, v, acc);
+      acc = i0 < A.norm_n ? fma(v, v, acc) : acc;
     }
   }
   const double p = block_sum(acc, red);
@@ -601,12 +605,12 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
       r.x = w.x - alpha * (rc.x * invN);
       r.y = w.y - alpha * (rc.y * invN);
       *reinterpret_cast<double2*>(r_next + i0) = r;
-      acc = fma(r.x, r.x, acc);
-      acc = fma(r.y, r.y, acc);
+      acc = i0 < A.norm_n ? fma(r.x, r.x, acc) : acc;
+      acc = i0 + 1 < A.norm_n ? fma(r.y, r.y, acc) : acc;
     } else {
       const double r = W[i0] - alpha * (r_cur[i0] * invN);
       r_next[i0] = r;
-      acc = fma(r, r, acc);
+      acc = i0 < A.norm_n ? fma(r, r, acc) : acc;
     }
   }
   const double p = block_sum(acc, red);
@@ -653,6 +657,78 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, 
   epi.Vcol = Vcol;
   double acc = 0.0;
   spmv_block<CW>(A, xsrc, UnitScale{}, epi, acc, lds);
+}
+
+// ---------------------------------------- replicated long rows (partitioned solve)
+// Long row l = sum over ranks, in rank order, of the R partials all-gathered into
+// yall[r * n_long + l]; every rank then runs the row's epilogue (identical bits on all
+// ranks). Local index of long row l: A.n - A.n_long + l. Alpha partial (pass one):
+// thread t accumulates fma(v, w) over rows t + 256q of its workgroup's range, tree256.
+template <class Epi>
+__device__ __forceinline__ double long_epi_rows(const CsrDev& A, const double* __restrict__ yall,
+                                                int R, const Epi& epi) {
+  double acc = 0.0;
+  const int l0 = blockIdx.x * kLongEpiRows;
+  const int l1 = l0 + kLongEpiRows < A.n_long ? l0 + kLongEpiRows : A.n_long;
+  const int base = (int)(A.n - A.n_long);
+  for (int l = l0 + threadIdx.x; l < l1; l += kTPB) {
+    const auto pre = epi.pre(base + l);
+    double y = 0.0;
+    for (int r = 0; r < R; ++r) y = y + yall[(size_t)r * A.n_long + l];
+    epi.apply(base + l, y, pre, acc);
+  }
+  return acc;
+}
+
+__global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
+                                                      const double* __restrict__ yall, int R,
+                                                      const double* __restrict__ r_cur,
+                                                      const double* __restrict__ r_prev,
+                                                      double* __restrict__ W,
+                                                      double* __restrict__ Vcol,
+                                                      double* __restrict__ Pa_long, int j) {
+  __shared__ double red[4];
+  if (S.flags[0]) return;  // stopped / breakdown (uniform)
+  const double beta = S.norms[j - 1];
+  EpiPass1 epi;
+  epi.r_cur = r_cur;
+  epi.r_prev = (j >= 2) ? r_prev : r_cur;
+  epi.has_prev = j >= 2;
+  epi.invN_cur = 1.0 / beta;
+  epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
+  epi.beta_sub = (j >= 2) ? beta : 0.0;
+  epi.W = W;
+  epi.Vcol = Vcol;
+  epi.Pa_long = nullptr;
+  const double acc = long_epi_rows(A, yall, R, epi);
+  const double p = block_sum(acc, red);
+  if (threadIdx.x == 0) Pa_long[blockIdx.x] = p;
+}
+
+__global__ __launch_bounds__(kTPB) void k_long_epi_y(CsrDev A, const double* __restrict__ yall,
+                                                     int R, double* __restrict__ y) {
+  long_epi_rows(A, yall, R, EpiSpmv{y});
+}
+
+__global__ __launch_bounds__(kTPB) void k_long_epi_p2(CsrDev A, DevState S,
+                                                      const double* __restrict__ yall, int R,
+                                                      const double* __restrict__ v_cur,
+                                                      const double* __restrict__ v_prev,
+                                                      double* __restrict__ v_next,
+                                                      double* __restrict__ x,
+                                                      double* __restrict__ Vcol, int j) {
+  EpiPass2 epi;
+  epi.v_cur = v_cur;
+  epi.v_prev = (j >= 2) ? v_prev : v_cur;
+  epi.has_prev = j >= 2;
+  epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
+  epi.alpha = S.alphas[j - 1];
+  epi.invb = 1.0 / S.betas[j - 1];
+  epi.ycoef = S.y[j];
+  epi.v_next = v_next;
+  epi.x = x;
+  epi.Vcol = Vcol;
+  long_epi_rows(A, yall, R, epi);
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
@@ -803,6 +879,28 @@ hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    hipStream_t s) {
   if (spmv_grid(A) > 0)
     TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j);
+  return hipGetLastError();
+}
+int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kLongEpiRows; }
+hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
+                       const double* r_cur, const double* r_prev, double* W, double* Vcol,
+                       double* Pa_long, int j, hipStream_t s) {
+  if (A.n_long > 0)
+    hipLaunchKernelGGL(k_long_epi_p1, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A, S, yall, R,
+                       r_cur, r_prev, W, Vcol, Pa_long, j);
+  return hipGetLastError();
+}
+hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hipStream_t s) {
+  if (A.n_long > 0)
+    hipLaunchKernelGGL(k_long_epi_y, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A, yall, R, y);
+  return hipGetLastError();
+}
+hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, int R,
+                       const double* v_cur, const double* v_prev, double* v_next, double* x,
+                       double* Vcol, int j, hipStream_t s) {
+  if (A.n_long > 0)
+    hipLaunchKernelGGL(k_long_epi_p2, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A, S, yall, R,
+                       v_cur, v_prev, v_next, x, Vcol, j);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,

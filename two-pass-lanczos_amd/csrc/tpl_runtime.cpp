@@ -40,6 +40,13 @@ hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    hipStream_t s);
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
                       hipStream_t s);
+hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
+                       const double* r_cur, const double* r_prev, double* W, double* Vcol,
+                       double* Pa_long, int j, hipStream_t s);
+hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, int R,
+                       const double* v_cur, const double* v_prev, double* v_next, double* x,
+                       double* Vcol, int j, hipStream_t s);
+hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hipStream_t s);
 hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
                       int64_t E, hipStream_t s);
 hipError_t reorth_reduce(int cols, const double* P, int G, double* h, hipStream_t s);
@@ -97,6 +104,7 @@ static tpl_status guarded(F&& f) {
 struct SchedParams {
   int short_row_max = -1;           // rows longer than this are sliced; -1 = auto
   int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
+  int64_t long_from = -1;           // >= 0: rows [long_from, n) are long, the rest short
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
@@ -142,7 +150,7 @@ static int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, in
 // partitioned over ranks, global column c (owned by rank r, rows [starts[r],
 // starts[r+1])) lives at r * ld + (c - starts[r]) of the all-gathered vector.
 struct ColMap {
-  const std::vector<int64_t>* starts = nullptr;  // nullptr: identity
+  const std::vector<int64_t>* starts = nullptr;  // row partition (nullptr: see table)
   int64_t ld = 0;
   int32_t operator()(int32_t c) const {
     if (!starts) return c;
@@ -161,7 +169,7 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
   Layout L;
   const int32_t T = short_row_threshold(n, rp, sp.short_row_max);
   for (int64_t i = 0; i < n; ++i) {
-    if (rp[i + 1] - rp[i] > T) L.lrows.push_back((int32_t)i);
+    if (sp.long_from >= 0 ? i >= sp.long_from : rp[i + 1] - rp[i] > T) L.lrows.push_back((int32_t)i);
     else L.srows.push_back((int32_t)i);
   }
   const int64_t ns = (int64_t)L.srows.size();
@@ -304,6 +312,13 @@ struct tpl_op_s {
   int64_t n_glob = 0;
   std::vector<int64_t> starts;
   bool eager = false;               // launch without graphs (host transport / no capture)
+  // replicated-long-row partition ("hybrid"): local vector = [own short rows | all long
+  // rows]; g2l maps global rows/columns to local indices (-1: not local), local_rows back
+  bool hybrid = false;
+  int64_t ns_local = 0;
+  std::vector<int32_t> g2l;
+  std::vector<int64_t> local_rows;
+  double* d_yall = nullptr;         // nranks x n_long long-row partials (all-gathered)
   std::vector<int32_t> h_rowptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
@@ -351,6 +366,10 @@ bool use_graphs() {
   return !(e && e[0] == '1');
 }
 
+int long_epi_blocks(const tpl_op_s* op) {
+  return (int)((op->lay.lrows.size() + kLongEpiRows - 1) / kLongEpiRows);
+}
+
 CsrDev csr_dev(const tpl_op_s* op) {
   const Layout& L = op->lay;
   CsrDev A;
@@ -372,8 +391,12 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.n_slice_blocks = kSlices * L.M;
   A.G2 = L.G2;
   A.NA = A.n_chunks + A.n_long;
-  A.NA_r = op->dist ? op->dist->nranks : A.NA;
+  A.NA_r = op->dist ? op->dist->nranks + (op->hybrid ? long_epi_blocks(op) : 0) : A.NA;
   A.G2_r = op->dist ? op->dist->nranks : A.G2;
+  A.long_defer = op->hybrid ? 1 : 0;
+  A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * L.lrows.size() : nullptr;
+  A.pad2 = 0;
+  A.norm_n = op->hybrid && op->dist->rank != 0 ? op->ns_local : op->n;
   A.pad = 0;
   A.n = op->n;
   A.E = L.E;
@@ -396,11 +419,14 @@ void upload(T** dst, const std::vector<T>& src) {
 
 void rebuild_schedule(tpl_op_s* op) {
   ColMap cmap;
-  if (op->dist) {
+  if (op->dist && !op->hybrid) {
     cmap.starts = &op->starts;
     cmap.ld = op->ld;
   }
-  op->lay = build_layout(op->n, op->n_glob, op->h_rowptr, op->h_col, op->h_val, op->sp, cmap);
+  // slice bounds over global columns — or, replicated-long-row partition, over this
+  // rank's local columns (its CSR is stored in local indices)
+  op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, op->h_rowptr, op->h_col,
+                         op->h_val, op->sp, cmap);
   const Layout& L = op->lay;
   upload(&op->d_srows, L.srows);
   upload(&op->d_scol, L.s_col);
@@ -445,7 +471,7 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->S.Pa = op->S.y + kc;
     op->S.Pb = op->S.Pa + std::max(A.NA, 1);
     op->S.Pa_r = op->dist ? op->d_rsum : op->S.Pa;
-    op->S.Pb_r = op->dist ? op->d_rsum + op->dist->nranks : op->S.Pb;
+    op->S.Pb_r = op->dist ? op->d_rsum + A.NA_r : op->S.Pb;
     op->kcap = kc;
   }
   if (reorth && !op->d_Pr) {
@@ -549,7 +575,10 @@ void enqueue_reorth(tpl_op_s* op, int j) {
 void enqueue_p1_prologue(tpl_op_s* op) {
   const CsrDev A = csr_dev(op);
   HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
-  if (op->dist) {
+  if (op->hybrid) {  // every column this rank gathers is local: only the norm totals move
+    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+    dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+  } else if (op->dist) {
     const int R = op->dist->nranks;
     dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
     dist_group(op, true);
@@ -564,6 +593,26 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
   const CsrDev A = csr_dev(op);
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
                          op->W, Vcol, j, op->stream));
+  if (op->hybrid) {
+    // short-row alpha total and the long rows' partials travel together; every rank then
+    // finishes the long rows itself (replicated) and adds their alpha once
+    const int R = op->dist->nranks;
+    const size_t nl = op->lay.lrows.size();
+    dist_total(op, op->S.Pa, A.n_chunks, op->d_rsum + op->dist->rank);
+    dist_group(op, true);
+    dist_allgather(op, op->d_rsum, 1);
+    if (nl) dist_allgather(op, op->d_yall, nl);
+    dist_group(op, false);
+    HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, R, r_of(op, j),
+                               j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol, op->d_rsum + R, j,
+                               op->stream));
+    HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
+    if (j < k) {
+      dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+      dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+    }
+    return;
+  }
   if (op->dist) {
     dist_total(op, op->S.Pa, A.NA, op->d_rsum + op->dist->rank);
     dist_allgather(op, op->d_rsum, 1);
@@ -590,7 +639,7 @@ void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
 
 void enqueue_pass2_init(tpl_op_s* op, double* Vout) {
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, op->stream));
-  if (op->dist) dist_allgather(op, op->V2G[1], (size_t)op->ld);
+  if (op->dist && !op->hybrid) dist_allgather(op, op->V2G[1], (size_t)op->ld);
 }
 void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
   const CsrDev A = csr_dev(op);
@@ -599,7 +648,15 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
     HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
                            Vcol, j, op->stream));
-    if (op->dist && j + 1 < (int)steps) dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
+    if (op->hybrid) {
+      const size_t nl = op->lay.lrows.size();
+      if (nl) dist_allgather(op, op->d_yall, nl);
+      HIPCHK(launch::long_epi_p2(A, op->S, op->d_yall, op->dist->nranks, op->V2[j % 3],
+                                 j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3],
+                                 op->x, Vcol, j, op->stream));
+    } else if (op->dist && j + 1 < (int)steps) {
+      dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
+    }
   }
 }
 void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
@@ -734,9 +791,9 @@ void zero_out(tpl_op_s* op, double* x_out, int mem) {
 // Layout, vectors and events of a freshly filled operator (single GPU or one rank
 // of a partition; the vector stride ld is common to all ranks).
 void init_op(tpl_op_s* op) {
-  const int R = op->dist ? op->dist->nranks : 1;
+  const int R = op->dist && !op->hybrid ? op->dist->nranks : 1;  // gathered vector copies
   int64_t widest = op->n;
-  if (op->dist)
+  if (op->dist && !op->hybrid)
     for (int r = 0; r < R; ++r) widest = std::max(widest, op->starts[r + 1] - op->starts[r]);
   op->ld = ((std::max<int64_t>(widest, 1) + 63) / 64) * 64;
   rebuild_schedule(op);
@@ -745,7 +802,8 @@ void init_op(tpl_op_s* op) {
   HIPCHK(hipMalloc(&op->d_vecs, (gathered + local) * sizeof(double)));
   HIPCHK(hipMemset(op->d_vecs, 0, (gathered + local) * sizeof(double)));
   double* p = op->d_vecs;
-  const size_t gl = (size_t)R * op->ld, own = (size_t)(op->dist ? op->dist->rank : 0) * op->ld;
+  const size_t gl = (size_t)R * op->ld;
+  const size_t own = (size_t)(op->dist && !op->hybrid ? op->dist->rank : 0) * op->ld;
   op->bG = p;
   p += gl;
   for (int i = 0; i < 3; ++i, p += gl) op->RG[i] = p;
@@ -760,12 +818,36 @@ void init_op(tpl_op_s* op) {
   for (int i = 0; i < 3; ++i) op->V2[i] = op->V2G[i] + own;
   op->tmp = op->tmpG + own;
   if (op->dist) {
-    HIPCHK(hipMalloc(&op->d_rsum, 2 * (size_t)R * sizeof(double)));
-    HIPCHK(hipMemset(op->d_rsum, 0, 2 * (size_t)R * sizeof(double)));
+    // [nranks alpha totals | long-row alpha partials (hybrid) | nranks norm totals]
+    const size_t nr = (size_t)op->dist->nranks;
+    const size_t cnt = 2 * nr + (op->hybrid ? (size_t)long_epi_blocks(op) : 0);
+    HIPCHK(hipMalloc(&op->d_rsum, cnt * sizeof(double)));
+    HIPCHK(hipMemset(op->d_rsum, 0, cnt * sizeof(double)));
+    if (op->hybrid) {
+      const size_t ya = std::max<size_t>(nr * op->lay.lrows.size(), 1);
+      HIPCHK(hipMalloc(&op->d_yall, ya * sizeof(double)));
+      HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
+    }
   }
   HIPCHK(hipEventCreate(&op->ev0));
   HIPCHK(hipEventCreate(&op->ev1));
   for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
+}
+
+// Contiguous blocks over items 0..m-1 with cost prefix[m+1]: cut where the prefix
+// crosses r/nranks of the total; every block keeps at least one item.
+void balanced_cuts(const std::vector<double>& prefix, int nranks, int64_t* starts) {
+  const int64_t m = (int64_t)prefix.size() - 1;
+  const double total = prefix[m];
+  starts[0] = 0;
+  int64_t i = 0;
+  for (int r = 1; r < nranks; ++r) {
+    const double target = total * r / nranks;
+    while (i < m && prefix[i] < target) ++i;
+    starts[r] = std::min<int64_t>(std::max<int64_t>(i, starts[r - 1] + 1), m - (nranks - r));
+    i = starts[r];
+  }
+  starts[nranks] = m;
 }
 
 } // namespace
@@ -863,6 +945,7 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
       if (p) hipFree(p);
     hipFree(op->d_vecs);
     if (op->d_rsum) hipFree(op->d_rsum);
+    if (op->d_yall) hipFree(op->d_yall);
     if (op->d_state) hipFree(op->d_state);
     if (op->h_state) hipHostFree(op->h_state);
     if (op->d_Pr) hipFree(op->d_Pr);
@@ -888,8 +971,13 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
     set_device(op);
     if (op->n == 0) return;
     upload_vec(op, op->tmp, x, mem);
-    if (op->dist) dist_allgather(op, op->tmpG, (size_t)op->ld);
-    HIPCHK(launch::spmv(csr_dev(op), op->tmpG, op->W, op->stream));
+    if (op->dist && !op->hybrid) dist_allgather(op, op->tmpG, (size_t)op->ld);
+    const CsrDev A = csr_dev(op);
+    HIPCHK(launch::spmv(A, op->tmpG, op->W, op->stream));
+    if (op->hybrid && A.n_long > 0) {
+      dist_allgather(op, op->d_yall, (size_t)A.n_long);
+      HIPCHK(launch::long_epi_y(A, op->d_yall, op->dist->nranks, op->W, op->stream));
+    }
     download_vec(op, y, op->W, op->n, mem);
     sync_checked(op);
   });
@@ -1195,20 +1283,11 @@ tpl_status tpl_dist_partition(int64_t n, const int64_t* row_ptr, int nranks, int
   return guarded([&] {
     if (!row_ptr || !starts || nranks < 1) fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
     if (n < nranks) fail(TPL_ERR_INVALID_ARGUMENT, "fewer rows than ranks");
-    // Contiguous row blocks balanced by algorithmic bytes: 12 per nonzero (value +
-    // column) + 40 per row (pass two's vector traffic), cut where the prefix crosses
-    // r/nranks of the total; every block keeps at least one row.
-    auto cost = [&](int64_t i) { return 12.0 * (double)row_ptr[i] + 40.0 * (double)i; };
-    const double total = cost(n);
-    starts[0] = 0;
-    int64_t i = 0;
-    for (int r = 1; r < nranks; ++r) {
-      const double target = total * r / nranks;
-      while (i < n && cost(i) < target) ++i;
-      starts[r] = std::min<int64_t>(std::max<int64_t>(i, starts[r - 1] + 1), n - (nranks - r));
-      i = starts[r];
-    }
-    starts[nranks] = n;
+    // contiguous row blocks balanced by algorithmic bytes: 12 per nonzero (value +
+    // column) + 40 per row (pass two's vector traffic)
+    std::vector<double> prefix(n + 1);
+    for (int64_t i = 0; i <= n; ++i) prefix[i] = 12.0 * (double)row_ptr[i] + 40.0 * (double)i;
+    balanced_cuts(prefix, nranks, starts);
   });
 }
 
@@ -1310,6 +1389,128 @@ tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t*
     op->h_val.assign(vals, vals + nnz);
     init_op(op.get());
     *out = op.release();
+  });
+}
+
+
+tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t* row_ptr,
+                                         const int32_t* col_idx, const double* vals,
+                                         tpl_op_t* out) {
+  return guarded([&] {
+    if (!d || !row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    const int R = d->nranks, me = d->rank;
+    const int64_t nnz = row_ptr[n];
+    if (n < 1 || n >= INT32_MAX / 2 || nnz >= INT32_MAX || row_ptr[0] != 0)
+      fail(TPL_ERR_INVALID_ARGUMENT, "bad CSR sizes");
+    if (nnz > 0 && (!col_idx || !vals)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    std::vector<int32_t> rp32(n + 1);
+    for (int64_t i = 0; i <= n; ++i) {
+      if (i > 0 && row_ptr[i] < row_ptr[i - 1]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
+      rp32[i] = (int32_t)row_ptr[i];
+    }
+    for (int64_t i = 0; i < n; ++i)
+      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q)
+        if (col_idx[q] < 0 || col_idx[q] >= n || (q > row_ptr[i] && col_idx[q] <= col_idx[q - 1]))
+          fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be in range and ascending per row");
+    // short / long rows by the global rule; long rows are replicated on every rank
+    const int32_t T = short_row_threshold(n, rp32, -1);
+    std::vector<int64_t> S, Lr;
+    std::vector<int32_t> lidx(n, -1);
+    for (int64_t i = 0; i < n; ++i) {
+      if (rp32[i + 1] - rp32[i] > T) {
+        lidx[i] = (int32_t)Lr.size();
+        Lr.push_back(i);
+      } else {
+        S.push_back(i);
+      }
+    }
+    if ((int64_t)S.size() < R) fail(TPL_ERR_UNSUPPORTED, "fewer short rows than ranks");
+    // short rows in contiguous blocks balanced by bytes: the row itself plus the
+    // long-row entries in its column, which the owner of that column computes
+    std::vector<int32_t> longcnt(n, 0);
+    for (int64_t l : Lr)
+      for (int64_t q = row_ptr[l]; q < row_ptr[l + 1]; ++q) longcnt[col_idx[q]]++;
+    std::vector<double> prefix(S.size() + 1, 0.0);
+    for (size_t p = 0; p < S.size(); ++p) {
+      const int64_t i = S[p];
+      prefix[p + 1] = prefix[p] + 12.0 * (double)(rp32[i + 1] - rp32[i] + longcnt[i]) + 40.0;
+    }
+    std::vector<int64_t> cut(R + 1);
+    balanced_cuts(prefix, R, cut.data());
+    std::vector<int32_t> owner(n, -1);
+    for (int r = 0; r < R; ++r)
+      for (int64_t p = cut[r]; p < cut[r + 1]; ++p) owner[S[p]] = r;
+    // halo-free check (all ranks decide alike: they all see the whole matrix)
+    for (int64_t i : S)
+      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+        const int32_t c = col_idx[q];
+        if (lidx[c] < 0 && owner[c] != owner[i])
+          fail(TPL_ERR_UNSUPPORTED, "a short row references a short row of another rank "
+                                    "(use the row-partitioned operator)");
+      }
+    HIPCHK(hipSetDevice(d->ctx.device));
+    auto op = std::make_unique<tpl_op_s>();
+    op->ctx = &d->ctx;
+    op->device = d->ctx.device;
+    op->stream = d->ctx.stream;
+    op->dist = d;
+    op->hybrid = true;
+    op->eager = d->comm == nullptr;
+    op->n_glob = n;
+    const int64_t ns = cut[me + 1] - cut[me], nl = (int64_t)Lr.size();
+    op->ns_local = ns;
+    op->n = ns + nl;
+    op->g2l.assign(n, -1);
+    op->local_rows.resize(op->n);
+    for (int64_t p = 0; p < ns; ++p) {
+      op->g2l[S[cut[me] + p]] = (int32_t)p;
+      op->local_rows[p] = S[cut[me] + p];
+    }
+    for (int64_t l = 0; l < nl; ++l) {
+      op->g2l[Lr[l]] = (int32_t)(ns + l);
+      op->local_rows[ns + l] = Lr[l];
+    }
+    // local CSR in local column indices, each row ascending: own short rows whole; long
+    // rows restricted to the columns this rank owns (long-row columns: rank 0). The
+    // long rows' 8 column slices then split this rank's own columns, so every XCD
+    // gets a share of the long-row work.
+    op->h_rowptr.assign(1, 0);
+    std::vector<std::pair<int32_t, double>> row;
+    for (int64_t p = 0; p < op->n; ++p) {
+      const int64_t i = op->local_rows[p];
+      const bool is_long = p >= ns;
+      row.clear();
+      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+        const int32_t c = col_idx[q];
+        if (is_long && !(lidx[c] < 0 ? owner[c] == me : me == 0)) continue;
+        row.emplace_back(op->g2l[c], vals[q]);
+      }
+      std::sort(row.begin(), row.end(),
+                [](const std::pair<int32_t, double>& a, const std::pair<int32_t, double>& b) {
+                  return a.first < b.first;
+                });
+      for (const auto& e : row) {
+        op->h_col.push_back(e.first);
+        op->h_val.push_back(e.second);
+      }
+      op->h_rowptr.push_back((int32_t)op->h_col.size());
+    }
+    op->nnz = (int64_t)op->h_col.size();
+    op->sp.long_from = ns;
+    init_op(op.get());
+    *out = op.release();
+  });
+}
+
+tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows) {
+  return guarded([&] {
+    if (!op || !rows) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (op->hybrid) {
+      std::copy(op->local_rows.begin(), op->local_rows.end(), rows);
+    } else {
+      const int64_t r0 = op->dist ? op->starts[op->dist->rank] : 0;
+      for (int64_t i = 0; i < op->n; ++i) rows[i] = r0 + i;
+    }
   });
 }
 

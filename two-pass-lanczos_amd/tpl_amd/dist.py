@@ -86,31 +86,54 @@ class DistContext:
 
 
 class DistHipCsrOp(HipCsrOp):
-    """This rank's block of rows of a symmetric A, resident in its GPU's HBM."""
+    """This rank's part of a symmetric A, resident in its GPU's HBM.
 
-    def __init__(self, a, ctx: DistContext, starts=None):
+    mode "replicated" (tpl_dist_op_create_replicated): short rows in byte-balanced
+    blocks, long rows replicated on every rank, n_long partials exchanged per SpMV;
+    mode "rows" (tpl_dist_op_create_csr): contiguous row blocks, the whole vector
+    all-gathered per SpMV; "auto": replicated when the matrix allows it (no short row
+    references another rank's short rows — the KKT case), else rows.
+    ``local_rows``: global row of each entry of this rank's vectors (``local(v)``).
+    """
+
+    def __init__(self, a, ctx: DistContext, starts=None, mode: str = "auto"):
         n, rp, ci, v = _as_csr_arrays(a)
-        self.starts = (partition((n, rp, ci, v), ctx.world) if starts is None
-                       else np.ascontiguousarray(starts, dtype=np.int64))
-        r0, r1 = int(self.starts[ctx.rank]), int(self.starts[ctx.rank + 1])
-        lrp = np.ascontiguousarray(rp[r0:r1 + 1] - rp[r0], dtype=np.int64)
-        lci = np.ascontiguousarray(ci[rp[r0]:rp[r1]], dtype=np.int32)
-        lv = np.ascontiguousarray(v[rp[r0]:rp[r1]], dtype=np.float64)
         self.device = ctx.device
         self.dist = ctx
-        self.row0, self.row1, self.n_global = r0, r1, n
+        self.n_global = n
         h = c_void_p()
-        check(_lib.tpl_dist_op_create_csr(
-            ctx.handle, n, self.starts.ctypes.data_as(POINTER(c_int64)),
-            lrp.ctypes.data_as(POINTER(c_int64)), lci.ctypes.data_as(POINTER(c_int32)),
-            lv.ctypes.data_as(POINTER(c_double)), byref(h)))
+        self.mode = None
+        if mode in ("auto", "replicated") and starts is None:
+            st = _lib.tpl_dist_op_create_replicated(
+                ctx.handle, n, rp.ctypes.data_as(POINTER(c_int64)),
+                ci.ctypes.data_as(POINTER(c_int32)), v.ctypes.data_as(POINTER(c_double)),
+                byref(h))
+            if st == _lib.TPL_OK:
+                self.mode = "replicated"
+            elif mode == "replicated" or st != _lib.TPL_ERR_UNSUPPORTED:
+                check(st)
+        if self.mode is None:
+            self.starts = (partition((n, rp, ci, v), ctx.world) if starts is None
+                           else np.ascontiguousarray(starts, dtype=np.int64))
+            r0, r1 = int(self.starts[ctx.rank]), int(self.starts[ctx.rank + 1])
+            lrp = np.ascontiguousarray(rp[r0:r1 + 1] - rp[r0], dtype=np.int64)
+            lci = np.ascontiguousarray(ci[rp[r0]:rp[r1]], dtype=np.int32)
+            lv = np.ascontiguousarray(v[rp[r0]:rp[r1]], dtype=np.float64)
+            check(_lib.tpl_dist_op_create_csr(
+                ctx.handle, n, self.starts.ctypes.data_as(POINTER(c_int64)),
+                lrp.ctypes.data_as(POINTER(c_int64)), lci.ctypes.data_as(POINTER(c_int32)),
+                lv.ctypes.data_as(POINTER(c_double)), byref(h)))
+            self.mode = "rows"
         self._op = h.value
-        self._n = r1 - r0
-        self._nnz = int(lrp[-1])
+        self._n = int(_lib.tpl_op_nrows(self._op))
+        self._nnz = int(_lib.tpl_op_nnz(self._op))
+        self.local_rows = np.zeros(max(self._n, 1), dtype=np.int64)
+        check(_lib.tpl_op_local_rows(self._op, self.local_rows.ctypes.data_as(POINTER(c_int64))))
+        self.local_rows = self.local_rows[:self._n]
 
     def ncols(self) -> int:
         return self.n_global
 
     def local(self, v):
-        """This rank's block of a global vector."""
-        return v[self.row0:self.row1]
+        """This rank's entries of a global vector."""
+        return v[self.local_rows]
