@@ -81,8 +81,13 @@ tpl_status tpl_op_destroy(tpl_op_t op);
 int64_t tpl_op_nrows(tpl_op_t op); /* LinOp::nrows / ncols */
 int64_t tpl_op_nnz(tpl_op_t op);
 /* Bit 0: row-partitioned operator; bit 1: passes launched eagerly (no hipGraph —
- * a host transport, or a transport that refused stream capture). -1 if op is NULL. */
+ * a host transport, or a transport that refused stream capture); bit 2: values kept
+ * as int8 (see tpl_op_set_value_format). -1 if op is NULL.                         */
 int tpl_op_flags(tpl_op_t op);
+/* Value format (rebuilds the layout): compress != 0 (default) keeps the values as
+ * int8 when every one is an integer in [-128, 127] (not -0.0) — lossless, results
+ * are bit-identical; 0 keeps fp64.                                                  */
+tpl_status tpl_op_set_value_format(tpl_op_t op, int compress);
 
 /* y = A x  — LinOp::apply (compatibility path; the solvers below keep the whole
  * recurrence on the device and never call this per step).                     */

@@ -373,3 +373,23 @@ def test_headline_500k_bitwise(kkt_tmp):
     xo, _ = o.pass_two(b, al, be, s, bn, ftk.INV(al, be) * bn)
     assert np.array_equal(x, xo)
     assert np.linalg.norm(a @ x - b) / np.linalg.norm(b) < 1e-8
+
+
+def test_int8_value_format_bitwise(kkt_tmp):
+    """Lossless value compression: the KKT's +-1 values are kept as int8 and every result
+    keeps its bits (tpl_op_set_value_format); non-integer values stay fp64."""
+    import tpl_amd
+    a = load_kkt(50000, kkt_tmp).a
+    b = harness_b(a)
+    op = tpl_amd.HipCsrOp(a)
+    assert op.int8_values
+    x8 = tpl_amd.lanczos_two_pass(op, b, 100, "exp")
+    d8 = tpl_amd.algorithms.lanczos_pass_one(op, b, 100)
+    op.set_value_format(False)
+    assert not op.int8_values
+    x64 = tpl_amd.lanczos_two_pass(op, b, 100, "exp")
+    d64 = tpl_amd.algorithms.lanczos_pass_one(op, b, 100)
+    assert np.array_equal(x8, x64)
+    assert np.array_equal(d8.alphas, d64.alphas) and np.array_equal(d8.betas, d64.betas)
+    op2 = tpl_amd.HipCsrOp(a * 0.5)
+    assert not op2.int8_values

@@ -57,7 +57,8 @@ constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB tab
 #ifndef TPL_BIN_MIN
 #define TPL_BIN_MIN 2048
 #endif
-constexpr int kBinMin = TPL_BIN_MIN; // default entries per bin (8 per thread)
+constexpr int kBinMin = TPL_BIN_MIN; // default entries per bin
+constexpr int kBinBatch = kBinMin / kTPB;  // entries per thread per load batch
 constexpr int kLongEpiRows = 1024;   // long rows per workgroup of k_long_epi_* (partitioned)
 constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
 // Slice partial slots hold this signalling-NaN bit pattern while empty (arithmetic
@@ -77,14 +78,15 @@ struct CsrDev {
   // short rows: sliced ELL
   const int32_t* srows;     // n_short short-row indices (ascending); unused if s_identity
   const int32_t* s_col;     // padded entries (col = -1 for padding)
-  const double* s_val;
+  const void* s_val;        // double, or int8_t when val_i8
   const int32_t* c_base;    // n_chunks chunk base offsets; unused if s_width > 0
   const int32_t* c_width;   // n_chunks chunk widths; unused if s_width > 0
   // long rows: bins (bin b = 8m + s holds pieces of slice s)
   const int32_t* b_col;     // n_bins x bin_cap entries (col = -1: padding)
-  const double* b_val;
+  const void* b_val;        // double, or int8_t when val_i8
   const BinSeg* b_seg;      // n_bins x kTPB table slots
   double* P;                // n_long x kSlices piece partials (sentinel when empty)
+  int32_t val_i8;           // 1: every stored value is a small integer, kept as int8
   int32_t s_width;          // > 0: every chunk has this width (bases computed)
   int32_t s_identity;       // 1: short rows are exactly 0 .. n_short-1
   int32_t n_short;

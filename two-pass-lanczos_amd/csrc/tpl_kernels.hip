@@ -211,10 +211,18 @@ struct UnitScale {
   __device__ __forceinline__ Scale operator()() const { return Scale{1.0, true}; }
 };
 
+// Matrix values: fp64, or int8 when every value is a small integer (V8 = 1; the
+// conversion to double is exact, so products and sums are bit-identical).
+template <int V8>
+__device__ __forceinline__ double val_at(const void* p, int i) {
+  if (V8) return (double)reinterpret_cast<const int8_t*>(p)[i];
+  return reinterpret_cast<const double*>(p)[i];
+}
+
 // ------------------------------------------------------ short rows (sliced ELL)
 // Chunk with a compile-time width W (entries loaded unconditionally: the sliced-ELL
 // storage is allocated for whole chunks, padding has col = -1).
-template <int W, class Epi, class ScaleFn>
+template <int W, int V8, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int base,
                                               const double* __restrict__ xsrc, ScaleFn scale_of,
                                               const Epi& epi, double& acc) {
@@ -239,7 +247,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
     for (int k = 0; k < W; ++k) {
       const int e = base + k * kChunkRows + q * kTPB + t;
       c[q][k] = A.s_col[e];
-      a[q][k] = A.s_val[e];
+      a[q][k] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.s_val, e);
     }
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q)
@@ -265,7 +273,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 // Any width (rare: chunks wider than 4). One row position at a time, entries in
 // batches of 8 with every load of a batch in flight; kept lean in registers, since a
 // kernel's VGPR budget is the maximum over all of its paths.
-template <class Epi, class ScaleFn>
+template <int V8, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int base, int W,
                                                 const double* __restrict__ xsrc, ScaleFn scale_of,
                                                 const Epi& epi, double& acc) {
@@ -288,7 +296,7 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
       for (int u = 0; u < 8; ++u) {
         const int e = base + clampi(k0 + u, W - 1) * kChunkRows + q * kTPB + t;
         c[u] = A.s_col[e];
-        a[u] = A.s_val[e];
+        a[u] = val_at<V8>(A.s_val, e);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
@@ -305,11 +313,12 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
 
 // CW > 0: the kernel was specialised for a uniform chunk width CW (tpl::launch picks
 // it from A.s_width); CW == 0: generic, any per-chunk width.
-template <int CW, class Epi, class ScaleFn>
+template <int CW, int V8, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
                                             const double* __restrict__ xsrc, ScaleFn scale_of,
                                             const Epi& epi, double& acc) {
-  if (CW > 0) return short_chunk_w<CW>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
+  if (CW > 0)
+    return short_chunk_w<CW, V8>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
   int W, base;
   if (A.s_width > 0) {
     W = A.s_width;
@@ -319,11 +328,11 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
     base = A.c_base[chunk];
   }
   switch (W) {
-    case 1: return short_chunk_w<1>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 2: return short_chunk_w<2>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 3: return short_chunk_w<3>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 4: return short_chunk_w<4>(A, chunk, base, xsrc, scale_of, epi, acc);
-    default: return short_chunk_any(A, chunk, base, W, xsrc, scale_of, epi, acc);
+    case 1: return short_chunk_w<1, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 2: return short_chunk_w<2, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 3: return short_chunk_w<3, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 4: return short_chunk_w<4, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
+    default: return short_chunk_any<V8>(A, chunk, base, W, xsrc, scale_of, epi, acc);
   }
 }
 
@@ -333,7 +342,7 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
 // then summed by one wave (lane-strided + butterfly) and handed back to thread j,
 // which owns piece j and publishes it; whoever completes a row's eight finalises it.
 // lds: bin_cap doubles of products, kTPB ints of piece starts, kTPB piece sums.
-template <class Epi, class ScaleFn>
+template <int V8, class Epi, class ScaleFn>
 __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                          const double* __restrict__ xsrc, ScaleFn scale_of,
                                          const Epi& epi, double* lds) {
@@ -341,32 +350,32 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   const int bin = m * kSlices + s;
   const BinSeg sg = A.b_seg[bin * kTPB + t];
   const int base = bin * A.bin_cap;
-  int c[8];
-  double a[8], xv[8];
+  int c[kBinBatch];
+  double a[kBinBatch], xv[kBinBatch];
 #pragma unroll
-  for (int u = 0; u < 8; ++u) {
+  for (int u = 0; u < kBinBatch; ++u) {
     c[u] = A.b_col[base + u * kTPB + t];
-    a[u] = A.b_val[base + u * kTPB + t];
+    a[u] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.b_val, base + u * kTPB + t);
   }
 #pragma unroll
-  for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
+  for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
   // the finalising thread's own row entries travel with the gathers
   const auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
   const Scale sc = scale_of();
   TPL_MARK(1);
   if (!sc.ok) return; // stopped / breakdown (uniform): slots untouched
 #pragma unroll
-  for (int u = 0; u < 8; ++u) lds[u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
-  for (int u0 = 8 * kTPB; u0 < A.bin_cap; u0 += 8 * kTPB) { // bins wider than 2048 (rare)
+  for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
+  for (int u0 = kBinBatch * kTPB; u0 < A.bin_cap; u0 += kBinBatch * kTPB) { // bins wider than one batch (rare)
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < kBinBatch; ++u) {
       c[u] = A.b_col[base + u0 + u * kTPB + t];
-      a[u] = A.b_val[base + u0 + u * kTPB + t];
+      a[u] = val_at<V8>(A.b_val, base + u0 + u * kTPB + t);
     }
 #pragma unroll
-    for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
+    for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
+    for (int u = 0; u < kBinBatch; ++u)
       lds[u0 + u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
   }
   int* starts = reinterpret_cast<int*>(lds + A.bin_cap);
@@ -444,42 +453,44 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
 #endif
 // Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
 // index whose alpha partial this workgroup owns, or -1.
-template <int CW, class Epi, class ScaleFn>
+// F = CW + 8 * V8: uniform chunk width (0: any) and the value format.
+template <int F, class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __restrict__ xsrc,
                                                ScaleFn scale_of, const Epi& epi, double& acc,
                                                double* lds) {
   int b = blockIdx.x;
   if (TPL_CHUNKS_FIRST) b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
   if (b < A.n_slice_blocks) {
-    if (!(TPL_ABLATE & 1)) long_bin(A, b / kSlices, b % kSlices, xsrc, scale_of, epi, lds);
+    if (!(TPL_ABLATE & 1))
+      long_bin<(F >> 3)>(A, b / kSlices, b % kSlices, xsrc, scale_of, epi, lds);
     return -1;
   }
   const int chunk = b - A.n_slice_blocks;
   if (TPL_ABLATE & 2) return -1;
-  return short_chunk<CW>(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
+  return short_chunk<(F & 7), (F >> 3)>(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
 }
 
-template <int CW, class Epi, class ScaleFn>
+template <int F, class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
                                           ScaleFn scale_of, const Epi& epi, double& acc,
                                           double* lds) {
 #if TPL_STAMP
   TPL_MARK(0);
-  const int r = spmv_block_impl<CW>(A, xsrc, scale_of, epi, acc, lds);
+  const int r = spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
   TPL_MARK(5);
   return r;
 #else
-  return spmv_block_impl<CW>(A, xsrc, scale_of, epi, acc, lds);
+  return spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
 #endif
 }
 
 // ------------------------------------------------------------------ kernels
-template <int CW>
+template <int F>
 __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_spmv(CsrDev A, const double* __restrict__ x,
                                                double* __restrict__ y) {
   extern __shared__ double lds[];
   double acc = 0.0;
-  spmv_block<CW>(A, x, UnitScale{}, EpiSpmv{y}, acc, lds);
+  spmv_block<F>(A, x, UnitScale{}, EpiSpmv{y}, acc, lds);
 }
 
 // Pass-one prologue: ||b||^2 partials, reset flags.
@@ -511,7 +522,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1), this rank's rows;
 // xsrc = the gather source holding r_j for every column (== r_cur on one GPU, the
 // all-gathered vector when the rows are partitioned over ranks).
-template <int CW>
+template <int F>
 __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ xsrc,
                                                   const double* __restrict__ r_cur,
@@ -557,7 +568,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
     return Scale{epi.invN_cur, true};
   };
   double acc = 0.0;
-  const int slot = spmv_block<CW>(A, xsrc, scale_fn, epi, acc, lds);
+  const int slot = spmv_block<F>(A, xsrc, scale_fn, epi, acc, lds);
   if (slot < 0) return; // uniform per workgroup
   const double p = block_sum(acc, red);
   if (threadIdx.x == 0) S.Pa[slot] = p;
@@ -635,7 +646,7 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
 }
 
 // Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x.
-template <int CW>
+template <int F>
 __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ xsrc,
                                                   const double* __restrict__ v_cur,
@@ -656,7 +667,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, 
   epi.x = x;
   epi.Vcol = Vcol;
   double acc = 0.0;
-  spmv_block<CW>(A, xsrc, UnitScale{}, epi, acc, lds);
+  spmv_block<F>(A, xsrc, UnitScale{}, epi, acc, lds);
 }
 
 // ---------------------------------------- replicated long rows (partitioned solve)
@@ -838,18 +849,23 @@ static inline size_t spmv_lds_bytes(const CsrDev& A) {
              : 0;
 }
 // Launch the SpMV-shaped kernel specialised for the layout's uniform chunk width.
+#define TPL_LAUNCH_CASE(KERNEL, F)                                                          \
+  case F: hipLaunchKernelGGL(KERNEL<F>, grid_, block_, shm_, s_, args_...); break
+// Launch the SpMV-shaped kernel specialised for the layout (chunk width, value format).
 #define TPL_LAUNCH_CW(KERNEL, A, s, ...)                                                    \
-  do {                                                                                      \
+  [&](auto... args_) {                                                                     \
     const dim3 grid_(spmv_grid(A)), block_(kTPB);                                           \
     const size_t shm_ = spmv_lds_bytes(A);                                                  \
-    switch ((A).s_width >= 1 && (A).s_width <= 4 ? (A).s_width : 0) {                       \
-      case 1: hipLaunchKernelGGL(KERNEL<1>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
-      case 2: hipLaunchKernelGGL(KERNEL<2>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
-      case 3: hipLaunchKernelGGL(KERNEL<3>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
-      case 4: hipLaunchKernelGGL(KERNEL<4>, grid_, block_, shm_, s, __VA_ARGS__); break;    \
-      default: hipLaunchKernelGGL(KERNEL<0>, grid_, block_, shm_, s, __VA_ARGS__); break;   \
+    hipStream_t s_ = (s);                                                                   \
+    const int cw_ = (A).s_width >= 1 && (A).s_width <= 4 ? (A).s_width : 0;                \
+    switch (cw_ + 8 * ((A).val_i8 ? 1 : 0)) {                                               \
+      TPL_LAUNCH_CASE(KERNEL, 0); TPL_LAUNCH_CASE(KERNEL, 1); TPL_LAUNCH_CASE(KERNEL, 2);   \
+      TPL_LAUNCH_CASE(KERNEL, 3); TPL_LAUNCH_CASE(KERNEL, 4); TPL_LAUNCH_CASE(KERNEL, 8);   \
+      TPL_LAUNCH_CASE(KERNEL, 9); TPL_LAUNCH_CASE(KERNEL, 10); TPL_LAUNCH_CASE(KERNEL, 11); \
+      TPL_LAUNCH_CASE(KERNEL, 12);                                                          \
+      default: break;                                                                       \
     }                                                                                       \
-  } while (0)
+  }(__VA_ARGS__)
 
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s) {
   if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_spmv, A, s, A, x, y);

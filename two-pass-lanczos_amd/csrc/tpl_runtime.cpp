@@ -105,6 +105,7 @@ struct SchedParams {
   int short_row_max = -1;           // rows longer than this are sliced; -1 = auto
   int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
   int64_t long_from = -1;           // >= 0: rows [long_from, n) are long, the rest short
+  bool compress_values = true;      // int8 values when all values are small integers
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
@@ -118,6 +119,8 @@ struct Layout {
   std::vector<int32_t> lrows;       // long rows, ascending
   std::vector<int32_t> b_col;       // long-row bins: n_bins x bin_cap entries
   std::vector<double> b_val;
+  bool val_i8 = false;              // every value a small integer: stored as int8
+  std::vector<int8_t> s_val8, b_val8;
   std::vector<BinSeg> b_seg;        // n_bins x kTPB table slots
   int32_t bin_cap = kBinMin;
   int32_t M = 0;                    // bins per slice
@@ -230,7 +233,7 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
                                   " nonzeros in one of its 8 column slices (limit " +
                                   std::to_string(kBinMax) + ")");
   L.bin_cap = std::max<int32_t>(kBinMin, ((widest + kTPB - 1) / kTPB) * kTPB);
-  L.bin_cap = ((L.bin_cap + 8 * kTPB - 1) / (8 * kTPB)) * (8 * kTPB);  // whole load batches
+  L.bin_cap = ((L.bin_cap + kBinMin - 1) / kBinMin) * kBinMin;  // whole load batches
   std::vector<std::vector<std::pair<int32_t, int32_t>>> bins[kSlices]; // (r, fill-at-start)
   std::vector<int32_t> fill[kSlices];
   for (int s = 0; s < kSlices && nl > 0; ++s) {
@@ -271,6 +274,21 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
           L.b_seg[bin * kTPB + j] = BinSeg{f, -1, -1, 0};
       }
     }
+  // Value compression: when every stored value (padding included) is an integer in
+  // [-128, 127] other than -0.0, keep int8 values; the device converts them back to
+  // double exactly, so every product and sum keeps its bits (the KKT values are +-1).
+  auto small_int = [](double v) {
+    return v >= -128.0 && v <= 127.0 && v == (double)(int8_t)v && !(v == 0.0 && std::signbit(v));
+  };
+  L.val_i8 = sp.compress_values;
+  for (double v : L.s_val) L.val_i8 = L.val_i8 && small_int(v);
+  for (double v : L.b_val) L.val_i8 = L.val_i8 && small_int(v);
+  if (L.val_i8) {
+    L.s_val8.assign(L.s_val.begin(), L.s_val.end());
+    L.b_val8.assign(L.b_val.begin(), L.b_val.end());
+    std::vector<double>().swap(L.s_val);
+    std::vector<double>().swap(L.b_val);
+  }
   const int64_t g2 = (n + 1023) / 1024;
   L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
   const int64_t per = (n + L.G2 - 1) / L.G2;
@@ -325,12 +343,12 @@ struct tpl_op_s {
   SchedParams sp;
   Layout lay;
   int32_t* d_bcol = nullptr;
-  double* d_bval = nullptr;
+  void* d_bval = nullptr;
   BinSeg* d_bseg = nullptr;
   double* d_P = nullptr;
   int32_t* d_srows = nullptr;
   int32_t* d_scol = nullptr;
-  double* d_sval = nullptr;
+  void* d_sval = nullptr;
   int32_t* d_cbase = nullptr;
   int32_t* d_cwidth = nullptr;
   // vectors: b, R0..R2, W, x, V2_0..V2_2, tmp (n each, padded)
@@ -376,6 +394,7 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.srows = op->d_srows;
   A.s_col = op->d_scol;
   A.s_val = op->d_sval;
+  A.val_i8 = L.val_i8 ? 1 : 0;
   A.c_base = op->d_cbase;
   A.c_width = op->d_cwidth;
   A.b_col = op->d_bcol;
@@ -430,11 +449,17 @@ void rebuild_schedule(tpl_op_s* op) {
   const Layout& L = op->lay;
   upload(&op->d_srows, L.srows);
   upload(&op->d_scol, L.s_col);
-  upload(&op->d_sval, L.s_val);
+  if (L.val_i8)
+    upload(reinterpret_cast<int8_t**>(&op->d_sval), L.s_val8);
+  else
+    upload(reinterpret_cast<double**>(&op->d_sval), L.s_val);
   upload(&op->d_cbase, L.c_base);
   upload(&op->d_cwidth, L.c_width);
   upload(&op->d_bcol, L.b_col);
-  upload(&op->d_bval, L.b_val);
+  if (L.val_i8)
+    upload(reinterpret_cast<int8_t**>(&op->d_bval), L.b_val8);
+  else
+    upload(reinterpret_cast<double**>(&op->d_bval), L.b_val);
   upload(&op->d_bseg, L.b_seg);
   // piece slots start empty (sentinel)
   std::vector<unsigned long long> empty(std::max<size_t>(L.lrows.size() * kSlices, 1),
@@ -961,7 +986,17 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
 int64_t tpl_op_nrows(tpl_op_t op) { return op ? op->n : -1; }
 int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
-  return (op->dist ? 1 : 0) | (op->eager ? 2 : 0);
+  return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0);
+}
+
+tpl_status tpl_op_set_value_format(tpl_op_t op, int compress) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    set_device(op);
+    op->sp.compress_values = compress != 0;
+    sync_checked(op);
+    rebuild_schedule(op);
+  });
 }
 int64_t tpl_op_nnz(tpl_op_t op) { return op ? op->nnz : -1; }
 

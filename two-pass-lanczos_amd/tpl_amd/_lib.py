@@ -86,6 +86,7 @@ tpl_op_destroy = _sig("tpl_op_destroy", c_int, c_void_p)
 tpl_op_nrows = _sig("tpl_op_nrows", c_int64, c_void_p)
 tpl_op_nnz = _sig("tpl_op_nnz", c_int64, c_void_p)
 tpl_op_flags = _sig("tpl_op_flags", c_int, c_void_p)
+tpl_op_set_value_format = _sig("tpl_op_set_value_format", c_int, c_void_p, c_int)
 tpl_op_apply = _sig("tpl_op_apply", c_int, c_void_p, c_void_p, c_void_p, c_int)
 tpl_lanczos = _sig("tpl_lanczos", c_int, c_void_p, c_void_p, c_int64, c_size_t, c_void_p,
                    c_void_p, c_void_p, c_int)
@@ -132,6 +133,7 @@ EXPORTED = [
     "tpl_lanczos_pass_two", "tpl_load_kkt_system", "tpl_csr_host_free", "tpl_op_schedule",
     "tpl_op_set_schedule", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
     "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_generate_kkt", "tpl_op_flags",
+    "tpl_op_set_value_format",
 ]
 
 

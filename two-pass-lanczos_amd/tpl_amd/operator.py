@@ -94,6 +94,14 @@ class HipCsrOp:
         return self._op
 
     @property
+    def int8_values(self) -> bool:
+        """True when the values are stored as int8 (lossless; tpl_op_set_value_format)."""
+        return bool(int(_lib.tpl_op_flags(self._op)) & 4)
+
+    def set_value_format(self, compress: bool):
+        check(_lib.tpl_op_set_value_format(self._op, 1 if compress else 0))
+
+    @property
     def uses_graphs(self) -> bool:
         """False when the passes are launched eagerly (see tpl_op_flags)."""
         return not (int(_lib.tpl_op_flags(self._op)) & 2)
