@@ -82,11 +82,13 @@ int64_t tpl_op_nrows(tpl_op_t op); /* LinOp::nrows / ncols */
 int64_t tpl_op_nnz(tpl_op_t op);
 /* Bit 0: row-partitioned operator; bit 1: passes launched eagerly (no hipGraph —
  * a host transport, or a transport that refused stream capture); bit 2: values kept
- * as int8 (see tpl_op_set_value_format). -1 if op is NULL.                         */
+ * as int8, bit 3 / bit 4: short-row / long-row column indices kept as uint16 offsets
+ * (see tpl_op_set_value_format). -1 if op is NULL.                                 */
 int tpl_op_flags(tpl_op_t op);
-/* Value format (rebuilds the layout): compress != 0 (default) keeps the values as
- * int8 when every one is an integer in [-128, 127] (not -0.0) — lossless, results
- * are bit-identical; 0 keeps fp64.                                                  */
+/* Storage format (rebuilds the layout): compress != 0 (default) keeps the values as
+ * int8 when every one is an integer in [-128, 127] (not -0.0), and the column
+ * indices as uint16 offsets from a per-chunk / per-bin base when the spans allow —
+ * lossless, results are bit-identical; 0 keeps fp64 values and int32 columns.       */
 tpl_status tpl_op_set_value_format(tpl_op_t op, int compress);
 
 /* y = A x  — LinOp::apply (compatibility path; the solvers below keep the whole

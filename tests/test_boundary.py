@@ -157,3 +157,11 @@ def test_netgen_fixture_regenerates_from_reference(tmp_path):
                          capture_output=True, check=True).stdout
     import hashlib
     assert hashlib.md5(out).hexdigest() == KKT_MD5[5000]
+
+
+def test_harness_rng_matches_oracle_restatement():
+    """The harness's StdRng (product utility) and the oracle's restatement agree."""
+    from tpl_amd.utils.rng import std_rng_f64
+    from oracle.rng import std_rng_vector
+    assert np.array_equal(std_rng_f64(10000, 42), std_rng_vector(10000, 42))
+    assert np.array_equal(std_rng_f64(7, 3), std_rng_vector(7, 3))

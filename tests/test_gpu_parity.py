@@ -383,10 +383,12 @@ def test_int8_value_format_bitwise(kkt_tmp):
     b = harness_b(a)
     op = tpl_amd.HipCsrOp(a)
     assert op.int8_values
+    from tpl_amd import _lib
+    assert int(_lib.tpl_op_flags(op.handle)) & 24 == 24  # uint16 columns in chunks and bins
     x8 = tpl_amd.lanczos_two_pass(op, b, 100, "exp")
     d8 = tpl_amd.algorithms.lanczos_pass_one(op, b, 100)
     op.set_value_format(False)
-    assert not op.int8_values
+    assert not op.int8_values and int(_lib.tpl_op_flags(op.handle)) & 24 == 0
     x64 = tpl_amd.lanczos_two_pass(op, b, 100, "exp")
     d64 = tpl_amd.algorithms.lanczos_pass_one(op, b, 100)
     assert np.array_equal(x8, x64)

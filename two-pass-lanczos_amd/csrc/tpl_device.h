@@ -77,16 +77,22 @@ struct BinSeg {
 struct CsrDev {
   // short rows: sliced ELL
   const int32_t* srows;     // n_short short-row indices (ascending); unused if s_identity
-  const int32_t* s_col;     // padded entries (col = -1 for padding)
+  const void* s_col;        // padded entries: int32 (col = -1 for padding), or uint16
+                            // offsets from s_cbase[chunk] (0xFFFF padding) when s_col16
+  const int32_t* s_cbase;   // per-chunk column base (s_col16)
   const void* s_val;        // double, or int8_t when val_i8
   const int32_t* c_base;    // n_chunks chunk base offsets; unused if s_width > 0
   const int32_t* c_width;   // n_chunks chunk widths; unused if s_width > 0
   // long rows: bins (bin b = 8m + s holds pieces of slice s)
-  const int32_t* b_col;     // n_bins x bin_cap entries (col = -1: padding)
+  const void* b_col;        // n_bins x bin_cap entries: int32 (-1: padding), or uint16
+                            // offsets from b_cbase[bin] (0xFFFF padding) when b_col16
+  const int32_t* b_cbase;   // per-bin column base (b_col16)
   const void* b_val;        // double, or int8_t when val_i8
   const BinSeg* b_seg;      // n_bins x kTPB table slots
   double* P;                // n_long x kSlices piece partials (sentinel when empty)
   int32_t val_i8;           // 1: every stored value is a small integer, kept as int8
+  int32_t s_col16;          // 1: chunk columns as uint16 offsets
+  int32_t b_col16;          // 1: bin columns as uint16 offsets
   int32_t s_width;          // > 0: every chunk has this width (bases computed)
   int32_t s_identity;       // 1: short rows are exactly 0 .. n_short-1
   int32_t n_short;

@@ -141,6 +141,11 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
   return block_sum(s, red);
 }
 
+// Pins a value as computed unconditionally: without it the compiler sinks the loads
+// feeding a product used under a select (padding entries) into a branch, where they
+// issue late behind an s_waitcnt vmcnt(0) and serialise the workgroup's round trips.
+__device__ __forceinline__ void keep(double& v) { asm volatile("" : "+v"(v)); }
+
 // ----------------------------------------------------------- epilogues
 // pre(i) loads the row's own vector entries (issued early); apply(i, s, pre, acc)
 // finishes the row given its SpMV sum s (acc: the thread's alpha accumulator).
@@ -202,6 +207,11 @@ struct EpiPass2 {
   __device__ __forceinline__ void long_alpha(int, double) const {}
 };
 
+// keep() for a row's epilogue inputs (used only for live rows / finalising threads)
+__device__ __forceinline__ void keep_pre(PreNone&) {}
+__device__ __forceinline__ void keep_pre(Pre1& p) { keep(p.rc); keep(p.rp); }
+__device__ __forceinline__ void keep_pre(Pre2& p) { keep(p.vc); keep(p.vp); keep(p.x); }
+
 // Result of a workgroup's prologue: the gather scale, or "stop" (uniform across the grid).
 struct Scale {
   double s;
@@ -219,14 +229,26 @@ __device__ __forceinline__ double val_at(const void* p, int i) {
   return reinterpret_cast<const double*>(p)[i];
 }
 
+// Column indices: int32 (padding -1), or — C16 — uint16 offsets from a per-chunk /
+// per-bin base (padding 0xFFFF) when every chunk / bin spans fewer than 65535 columns.
+template <int C16>
+__device__ __forceinline__ int col_at(const void* p, int i, int base) {
+  if (C16) {
+    const int off = reinterpret_cast<const uint16_t*>(p)[i];
+    return off == 0xFFFF ? -1 : base + off;
+  }
+  return reinterpret_cast<const int32_t*>(p)[i];
+}
+
 // ------------------------------------------------------ short rows (sliced ELL)
 // Chunk with a compile-time width W (entries loaded unconditionally: the sliced-ELL
 // storage is allocated for whole chunks, padding has col = -1).
-template <int W, int V8, class Epi, class ScaleFn>
+template <int W, int V8, int C16, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int base,
                                               const double* __restrict__ xsrc, ScaleFn scale_of,
                                               const Epi& epi, double& acc) {
   const int t = threadIdx.x;
+  const int cbase = C16 ? A.s_cbase[chunk] : 0;
   int row[kRowsPerThread];
   bool live[kRowsPerThread];
   decltype(epi.pre(0)) pre[kRowsPerThread];
@@ -246,7 +268,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 #pragma unroll
     for (int k = 0; k < W; ++k) {
       const int e = base + k * kChunkRows + q * kTPB + t;
-      c[q][k] = A.s_col[e];
+      c[q][k] = col_at<C16>(A.s_col, e, cbase);
       a[q][k] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.s_val, e);
     }
 #pragma unroll
@@ -257,12 +279,15 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
   TPL_MARK(1);
   if (!sc.ok) return false; // stopped / breakdown (uniform)
 #pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) keep_pre(pre[q]);
+#pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) {
     double sum = 0.0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-      const double nxt = sum + a[q][k] * (xv[q][k] * sc.s);
-      sum = c[q][k] >= 0 ? nxt : sum;
+      double prod = a[q][k] * (xv[q][k] * sc.s);
+      keep(prod);
+      sum = c[q][k] >= 0 ? sum + prod : sum;
     }
     if (live[q]) epi.apply(row[q], sum, pre[q], acc);
   }
@@ -273,11 +298,12 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 // Any width (rare: chunks wider than 4). One row position at a time, entries in
 // batches of 8 with every load of a batch in flight; kept lean in registers, since a
 // kernel's VGPR budget is the maximum over all of its paths.
-template <int V8, class Epi, class ScaleFn>
+template <int V8, int C16, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int base, int W,
                                                 const double* __restrict__ xsrc, ScaleFn scale_of,
                                                 const Epi& epi, double& acc) {
   const int t = threadIdx.x;
+  const int cbase = C16 ? A.s_cbase[chunk] : 0;
   const Scale sc = scale_of();
   if (!sc.ok) return false;
 #pragma unroll 1
@@ -286,7 +312,7 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
     const bool live = p < A.n_short;
     const int pc = clampi(p, A.n_short - 1);
     const int row = A.s_identity ? pc : A.srows[pc];
-    const auto pre = epi.pre(row);
+    auto pre = epi.pre(row);
     double s = 0.0;
 #pragma unroll 1
     for (int k0 = 0; k0 < W; k0 += 8) {
@@ -295,17 +321,19 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         const int e = base + clampi(k0 + u, W - 1) * kChunkRows + q * kTPB + t;
-        c[u] = A.s_col[e];
+        c[u] = col_at<C16>(A.s_col, e, cbase);
         a[u] = val_at<V8>(A.s_val, e);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const double nxt = s + a[u] * (xv[u] * sc.s);
-        s = (c[u] >= 0 && k0 + u < W) ? nxt : s;
+        double prod = a[u] * (xv[u] * sc.s);
+        keep(prod);
+        s = (c[u] >= 0 && k0 + u < W) ? s + prod : s;
       }
     }
+    keep_pre(pre);
     if (live) epi.apply(row, s, pre, acc);
   }
   return true;
@@ -313,12 +341,12 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
 
 // CW > 0: the kernel was specialised for a uniform chunk width CW (tpl::launch picks
 // it from A.s_width); CW == 0: generic, any per-chunk width.
-template <int CW, int V8, class Epi, class ScaleFn>
+template <int CW, int V8, int C16, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
                                             const double* __restrict__ xsrc, ScaleFn scale_of,
                                             const Epi& epi, double& acc) {
   if (CW > 0)
-    return short_chunk_w<CW, V8>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
+    return short_chunk_w<CW, V8, C16>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
   int W, base;
   if (A.s_width > 0) {
     W = A.s_width;
@@ -328,11 +356,11 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
     base = A.c_base[chunk];
   }
   switch (W) {
-    case 1: return short_chunk_w<1, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 2: return short_chunk_w<2, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 3: return short_chunk_w<3, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 4: return short_chunk_w<4, V8>(A, chunk, base, xsrc, scale_of, epi, acc);
-    default: return short_chunk_any<V8>(A, chunk, base, W, xsrc, scale_of, epi, acc);
+    case 1: return short_chunk_w<1, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 2: return short_chunk_w<2, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 3: return short_chunk_w<3, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 4: return short_chunk_w<4, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
+    default: return short_chunk_any<V8, C16>(A, chunk, base, W, xsrc, scale_of, epi, acc);
   }
 }
 
@@ -342,7 +370,7 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
 // then summed by one wave (lane-strided + butterfly) and handed back to thread j,
 // which owns piece j and publishes it; whoever completes a row's eight finalises it.
 // lds: bin_cap doubles of products, kTPB ints of piece starts, kTPB piece sums.
-template <int V8, class Epi, class ScaleFn>
+template <int V8, int C16, class Epi, class ScaleFn>
 __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                          const double* __restrict__ xsrc, ScaleFn scale_of,
                                          const Epi& epi, double* lds) {
@@ -350,33 +378,38 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   const int bin = m * kSlices + s;
   const BinSeg sg = A.b_seg[bin * kTPB + t];
   const int base = bin * A.bin_cap;
+  const int cbase = C16 ? A.b_cbase[bin] : 0;
   int c[kBinBatch];
   double a[kBinBatch], xv[kBinBatch];
 #pragma unroll
   for (int u = 0; u < kBinBatch; ++u) {
-    c[u] = A.b_col[base + u * kTPB + t];
+    c[u] = col_at<C16>(A.b_col, base + u * kTPB + t, cbase);
     a[u] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.b_val, base + u * kTPB + t);
   }
 #pragma unroll
   for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
   // the finalising thread's own row entries travel with the gathers
-  const auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
+  auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
   const Scale sc = scale_of();
   TPL_MARK(1);
   if (!sc.ok) return; // stopped / breakdown (uniform): slots untouched
+  // padding slots (col = -1) are never summed (pieces cover real entries only), so the
+  // product is stored unconditionally: a select here lets the compiler sink the loads
+  // of that entry into a branch and serialise them behind everything else in flight
 #pragma unroll
-  for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
+  for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = a[u] * (xv[u] * sc.s);
+  keep_pre(pre);
   for (int u0 = kBinBatch * kTPB; u0 < A.bin_cap; u0 += kBinBatch * kTPB) { // bins wider than one batch (rare)
 #pragma unroll
     for (int u = 0; u < kBinBatch; ++u) {
-      c[u] = A.b_col[base + u0 + u * kTPB + t];
+      c[u] = col_at<C16>(A.b_col, base + u0 + u * kTPB + t, cbase);
       a[u] = val_at<V8>(A.b_val, base + u0 + u * kTPB + t);
     }
 #pragma unroll
     for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
 #pragma unroll
     for (int u = 0; u < kBinBatch; ++u)
-      lds[u0 + u * kTPB + t] = c[u] >= 0 ? a[u] * (xv[u] * sc.s) : 0.0;
+      lds[u0 + u * kTPB + t] = a[u] * (xv[u] * sc.s);
   }
   int* starts = reinterpret_cast<int*>(lds + A.bin_cap);
   double* psum = lds + A.bin_cap + kTPB / 2;  // kTPB doubles after the starts
@@ -453,7 +486,8 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
 #endif
 // Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
 // index whose alpha partial this workgroup owns, or -1.
-// F = CW + 8 * V8: uniform chunk width (0: any) and the value format.
+// F = CW | V8 << 3 | SC16 << 4 | BC16 << 5: uniform chunk width (0: any), int8 values,
+// uint16 column offsets in the chunks / in the bins.
 template <int F, class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __restrict__ xsrc,
                                                ScaleFn scale_of, const Epi& epi, double& acc,
@@ -462,12 +496,13 @@ __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __
   if (TPL_CHUNKS_FIRST) b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
   if (b < A.n_slice_blocks) {
     if (!(TPL_ABLATE & 1))
-      long_bin<(F >> 3)>(A, b / kSlices, b % kSlices, xsrc, scale_of, epi, lds);
+      long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / kSlices, b % kSlices, xsrc, scale_of, epi, lds);
     return -1;
   }
   const int chunk = b - A.n_slice_blocks;
   if (TPL_ABLATE & 2) return -1;
-  return short_chunk<(F & 7), (F >> 3)>(A, chunk, xsrc, scale_of, epi, acc) ? chunk : -1;
+  return short_chunk<(F & 7), ((F >> 3) & 1), ((F >> 4) & 1)>(A, chunk, xsrc, scale_of, epi, acc)
+             ? chunk : -1;
 }
 
 template <int F, class Epi, class ScaleFn>
@@ -858,12 +893,18 @@ static inline size_t spmv_lds_bytes(const CsrDev& A) {
     const size_t shm_ = spmv_lds_bytes(A);                                                  \
     hipStream_t s_ = (s);                                                                   \
     const int cw_ = (A).s_width >= 1 && (A).s_width <= 4 ? (A).s_width : 0;                \
-    switch (cw_ + 8 * ((A).val_i8 ? 1 : 0)) {                                               \
-      TPL_LAUNCH_CASE(KERNEL, 0); TPL_LAUNCH_CASE(KERNEL, 1); TPL_LAUNCH_CASE(KERNEL, 2);   \
-      TPL_LAUNCH_CASE(KERNEL, 3); TPL_LAUNCH_CASE(KERNEL, 4); TPL_LAUNCH_CASE(KERNEL, 8);   \
-      TPL_LAUNCH_CASE(KERNEL, 9); TPL_LAUNCH_CASE(KERNEL, 10); TPL_LAUNCH_CASE(KERNEL, 11); \
-      TPL_LAUNCH_CASE(KERNEL, 12);                                                          \
-      default: break;                                                                       \
+    switch (cw_ | ((A).val_i8 ? 8 : 0) | ((A).s_col16 ? 16 : 0) | ((A).b_col16 ? 32 : 0)) { \
+      TPL_LAUNCH_CASE(KERNEL, 0); TPL_LAUNCH_CASE(KERNEL, 32); TPL_LAUNCH_CASE(KERNEL, 16); TPL_LAUNCH_CASE(KERNEL, 48);\
+      TPL_LAUNCH_CASE(KERNEL, 8); TPL_LAUNCH_CASE(KERNEL, 40); TPL_LAUNCH_CASE(KERNEL, 24); TPL_LAUNCH_CASE(KERNEL, 56);\
+      TPL_LAUNCH_CASE(KERNEL, 1); TPL_LAUNCH_CASE(KERNEL, 33); TPL_LAUNCH_CASE(KERNEL, 17); TPL_LAUNCH_CASE(KERNEL, 49);\
+      TPL_LAUNCH_CASE(KERNEL, 9); TPL_LAUNCH_CASE(KERNEL, 41); TPL_LAUNCH_CASE(KERNEL, 25); TPL_LAUNCH_CASE(KERNEL, 57);\
+      TPL_LAUNCH_CASE(KERNEL, 2); TPL_LAUNCH_CASE(KERNEL, 34); TPL_LAUNCH_CASE(KERNEL, 18); TPL_LAUNCH_CASE(KERNEL, 50);\
+      TPL_LAUNCH_CASE(KERNEL, 10); TPL_LAUNCH_CASE(KERNEL, 42); TPL_LAUNCH_CASE(KERNEL, 26); TPL_LAUNCH_CASE(KERNEL, 58);\
+      TPL_LAUNCH_CASE(KERNEL, 3); TPL_LAUNCH_CASE(KERNEL, 35); TPL_LAUNCH_CASE(KERNEL, 19); TPL_LAUNCH_CASE(KERNEL, 51);\
+      TPL_LAUNCH_CASE(KERNEL, 11); TPL_LAUNCH_CASE(KERNEL, 43); TPL_LAUNCH_CASE(KERNEL, 27); TPL_LAUNCH_CASE(KERNEL, 59);\
+      TPL_LAUNCH_CASE(KERNEL, 4); TPL_LAUNCH_CASE(KERNEL, 36); TPL_LAUNCH_CASE(KERNEL, 20); TPL_LAUNCH_CASE(KERNEL, 52);\
+      TPL_LAUNCH_CASE(KERNEL, 12); TPL_LAUNCH_CASE(KERNEL, 44); TPL_LAUNCH_CASE(KERNEL, 28); TPL_LAUNCH_CASE(KERNEL, 60);\
+      default: break;                                                                   \
     }                                                                                       \
   }(__VA_ARGS__)
 

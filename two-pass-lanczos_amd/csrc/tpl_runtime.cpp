@@ -106,6 +106,7 @@ struct SchedParams {
   int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
   int64_t long_from = -1;           // >= 0: rows [long_from, n) are long, the rest short
   bool compress_values = true;      // int8 values when all values are small integers
+  bool compress_cols = true;        // uint16 column offsets when the spans allow
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
@@ -121,6 +122,9 @@ struct Layout {
   std::vector<double> b_val;
   bool val_i8 = false;              // every value a small integer: stored as int8
   std::vector<int8_t> s_val8, b_val8;
+  bool s_col16 = false, b_col16 = false;  // uint16 column offsets from a per-chunk/bin base
+  std::vector<uint16_t> s_col16v, b_col16v;
+  std::vector<int32_t> s_cbase, b_cbase;
   std::vector<BinSeg> b_seg;        // n_bins x kTPB table slots
   int32_t bin_cap = kBinMin;
   int32_t M = 0;                    // bins per slice
@@ -289,6 +293,34 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
     std::vector<double>().swap(L.s_val);
     std::vector<double>().swap(L.b_val);
   }
+  // Column compression: uint16 offsets from each chunk's / bin's smallest column when
+  // every chunk / bin spans fewer than 65535 columns (0xFFFF marks padding).
+  auto compress_cols = [&](const std::vector<int32_t>& cols, int64_t groups, int64_t per,
+                           std::vector<uint16_t>& out16, std::vector<int32_t>& base) {
+    if (!sp.compress_cols || groups == 0) return false;
+    base.assign(groups, 0);
+    for (int64_t g = 0; g < groups; ++g) {
+      int32_t lo = INT32_MAX, hi = -1;
+      for (int64_t e = g * per; e < (g + 1) * per && e < (int64_t)cols.size(); ++e)
+        if (cols[e] >= 0) {
+          lo = std::min(lo, cols[e]);
+          hi = std::max(hi, cols[e]);
+        }
+      if (hi < 0) lo = hi = 0;
+      if (hi - lo >= 0xFFFF) return false;
+      base[g] = lo;
+    }
+    out16.resize(cols.size());
+    for (size_t e = 0; e < cols.size(); ++e)
+      out16[e] = cols[e] < 0 ? 0xFFFF : (uint16_t)(cols[e] - base[e / per]);
+    return true;
+  };
+  // chunks have a uniform stride only when the widths are uniform (else per-chunk bases)
+  if (L.s_width > 0)
+    L.s_col16 = compress_cols(L.s_col, nchunks, (int64_t)L.s_width * kChunkRows, L.s_col16v, L.s_cbase);
+  L.b_col16 = compress_cols(L.b_col, (int64_t)kSlices * L.M, L.bin_cap, L.b_col16v, L.b_cbase);
+  if (L.s_col16) std::vector<int32_t>().swap(L.s_col);
+  if (L.b_col16) std::vector<int32_t>().swap(L.b_col);
   const int64_t g2 = (n + 1023) / 1024;
   L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
   const int64_t per = (n + L.G2 - 1) / L.G2;
@@ -342,12 +374,14 @@ struct tpl_op_s {
   std::vector<double> h_val;
   SchedParams sp;
   Layout lay;
-  int32_t* d_bcol = nullptr;
+  void* d_bcol = nullptr;
+  int32_t* d_bcbase = nullptr;
+  int32_t* d_scbase = nullptr;
   void* d_bval = nullptr;
   BinSeg* d_bseg = nullptr;
   double* d_P = nullptr;
   int32_t* d_srows = nullptr;
-  int32_t* d_scol = nullptr;
+  void* d_scol = nullptr;
   void* d_sval = nullptr;
   int32_t* d_cbase = nullptr;
   int32_t* d_cwidth = nullptr;
@@ -395,6 +429,10 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.s_col = op->d_scol;
   A.s_val = op->d_sval;
   A.val_i8 = L.val_i8 ? 1 : 0;
+  A.s_col16 = L.s_col16 ? 1 : 0;
+  A.b_col16 = L.b_col16 ? 1 : 0;
+  A.s_cbase = op->d_scbase;
+  A.b_cbase = op->d_bcbase;
   A.c_base = op->d_cbase;
   A.c_width = op->d_cwidth;
   A.b_col = op->d_bcol;
@@ -448,14 +486,22 @@ void rebuild_schedule(tpl_op_s* op) {
                          op->h_val, op->sp, cmap);
   const Layout& L = op->lay;
   upload(&op->d_srows, L.srows);
-  upload(&op->d_scol, L.s_col);
+  if (L.s_col16)
+    upload(reinterpret_cast<uint16_t**>(&op->d_scol), L.s_col16v);
+  else
+    upload(reinterpret_cast<int32_t**>(&op->d_scol), L.s_col);
+  upload(&op->d_scbase, L.s_cbase);
   if (L.val_i8)
     upload(reinterpret_cast<int8_t**>(&op->d_sval), L.s_val8);
   else
     upload(reinterpret_cast<double**>(&op->d_sval), L.s_val);
   upload(&op->d_cbase, L.c_base);
   upload(&op->d_cwidth, L.c_width);
-  upload(&op->d_bcol, L.b_col);
+  if (L.b_col16)
+    upload(reinterpret_cast<uint16_t**>(&op->d_bcol), L.b_col16v);
+  else
+    upload(reinterpret_cast<int32_t**>(&op->d_bcol), L.b_col);
+  upload(&op->d_bcbase, L.b_cbase);
   if (L.val_i8)
     upload(reinterpret_cast<int8_t**>(&op->d_bval), L.b_val8);
   else
@@ -965,6 +1011,7 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipStreamSynchronize(op->stream);
     drop_graphs(op);
     for (void* p : {(void*)op->d_bcol, (void*)op->d_bval, (void*)op->d_bseg, (void*)op->d_P,
+                    (void*)op->d_bcbase, (void*)op->d_scbase,
                     (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval,
                     (void*)op->d_cbase, (void*)op->d_cwidth})
       if (p) hipFree(p);
@@ -986,7 +1033,8 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
 int64_t tpl_op_nrows(tpl_op_t op) { return op ? op->n : -1; }
 int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
-  return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0);
+  return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0) |
+         (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0);
 }
 
 tpl_status tpl_op_set_value_format(tpl_op_t op, int compress) {
@@ -994,6 +1042,7 @@ tpl_status tpl_op_set_value_format(tpl_op_t op, int compress) {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     set_device(op);
     op->sp.compress_values = compress != 0;
+    op->sp.compress_cols = compress != 0;
     sync_checked(op);
     rebuild_schedule(op);
   });
