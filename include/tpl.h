@@ -195,8 +195,9 @@ tpl_status tpl_generate_kkt(int64_t num_arcs, int64_t num_nodes, uint64_t seed,
 /* ---- introspection / measurement ---------------------------------------- */
 /* SpMV layout of the operator (DESIGN.md "SpMV layout"): rows with at most
  * short_row_max nnz ("short", ascending) are stored as sliced ELL, 1024 rows per
- * chunk, one workgroup each; the n_long longer rows (ascending) are cut into 8
- * column slices handled by XCD-local workgroups and summed by the last arriver.
+ * chunk, one workgroup each; the n_long longer rows (ascending) are cut into S
+ * column slices (tpl_op_slices) handled by XCD-local workgroups and summed by the
+ * last arriver.
  * G2 workgroups of E elements run the element-wise kernels (= #norm partials).
  * short_rows_out: n_short int32 or NULL; long_rows_out: n_long int32 or NULL.
  * The CPU oracle uses this to reproduce the device reduction order bit for bit.   */
@@ -206,6 +207,12 @@ tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_short, int32_t* n_long, int32
  * -1: the default auto rule T = clamp(2 * median row nnz, 4, 32)), max_g2
  * (default 1024).                                                                */
 tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g2);
+/* Column slices S of the long rows (1, 2, 4 or 8; part of the canonical reduction
+ * order). tpl_op_set_slices rebuilds the layout with an explicit S
+ * (0 = the auto rule: the fewest slices whose share of the vector fits half an L2,
+ * more if a (row, slice) piece would not fit one bin).                          */
+tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices);
+tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices);
 
 /* Live timing of the solver's own launches: with timing on, HIP events on the
  * operator's stream bracket pass one's graph and the graph of pass two's step

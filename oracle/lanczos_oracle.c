@@ -50,11 +50,10 @@ typedef struct {
   const int32_t* lrows;  /* long rows (column slices), ascending */
   int32_t G2;            /* element-wise workgroups == #norm partials */
   int64_t E;             /* elements per element-wise workgroup */
+  int32_t slices;        /* column slices S of the long rows (1, 2, 4, 8) */
 } osched;
 
 #define CHUNK 512        /* short-row positions per sliced-ELL chunk (kChunkRows) */
-
-#define SLICES 8
 
 /* ------------------------------------------------------------ trees */
 static double tree64(double* a) { /* xor butterfly, offsets 1, 2, 4, 8, 16, 32 */
@@ -91,28 +90,39 @@ static void spmv_faithful(const ocsr* A, const double* x, double* y) {
   }
 }
 
-/* long row: per slice s (columns [floor(n*s/8), floor(n*(s+1)/8))) lane g (0..7)
- * sums the slice's entries g + 8q; butterfly over the 8 lanes (xor 1, 2, 4) -> P_s;
- * y = 0; y += P_s (s ascending). */
-static double long_row_canon(const ocsr* A, int32_t i, const double* x) {
+/* long row: per slice s (columns [floor(n*s/S), floor(n*(s+1)/S))) the slice's entries
+ * form a piece; a piece of at most BIG_PIECE entries: lane g (0..7) sums its entries
+ * g + 8q, butterfly over the 8 lanes (xor 1, 2, 4); a longer piece: lane l (0..63) sums
+ * its entries l + 64q, tree64. -> P_s; y = 0; y += P_s (s ascending). S: the
+ * schedule's slice count (tpl_runtime.cpp auto_slices).
+ * (device: long_bin in tpl_kernels.hip; kBigPiece in tpl_device.h) */
+#define BIG_PIECE 64
+static double long_row_canon(const ocsr* A, int32_t i, const double* x, int S) {
   const int64_t n = A->n;
   int64_t q = A->rp[i];
   double y = 0.0;
-  for (int s = 0; s < SLICES; ++s) {
-    const int64_t bound = (s + 1 == SLICES) ? INT64_MAX : n * (s + 1) / SLICES;
+  for (int s = 0; s < S; ++s) {
+    const int64_t bound = (s + 1 == S) ? INT64_MAX : n * (s + 1) / S;
     int64_t e = q;
     while (e < A->rp[i + 1] && A->ci[e] < bound) ++e;
-    double lane[8], nx[8];
-    for (int g = 0; g < 8; ++g) {
+    const int G = (e - q > BIG_PIECE) ? 64 : 8;
+    double lane[64], nx[64];
+    for (int g = 0; g < G; ++g) {
       double p = 0.0;
-      for (int64_t k = q + g; k < e; k += 8) p = p + A->v[k] * x[A->ci[k]];
+      for (int64_t k = q + g; k < e; k += G) p = p + A->v[k] * x[A->ci[k]];
       lane[g] = p;
     }
-    for (int h = 1; h < 8; h <<= 1) {
-      for (int g = 0; g < 8; ++g) nx[g] = lane[g] + lane[g ^ h];
-      memcpy(lane, nx, sizeof(nx));
+    double ps;
+    if (G == 64) {
+      ps = tree64(lane);
+    } else {
+      for (int h = 1; h < 8; h <<= 1) {
+        for (int g = 0; g < 8; ++g) nx[g] = lane[g] + lane[g ^ h];
+        memcpy(lane, nx, 8 * sizeof(double));
+      }
+      ps = lane[0];
     }
-    y = y + lane[0];
+    y = y + ps;
     q = e;
   }
   return y;
@@ -125,7 +135,7 @@ static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* 
     for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
     y[i] = s;
   }
-  for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_canon(A, S->lrows[r], x);
+  for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_canon(A, S->lrows[r], x, S->slices);
 }
 
 static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {

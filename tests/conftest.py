@@ -106,4 +106,28 @@ def canon_schedule(a, short_row_max=-1, max_g2=1024):
     g2 = max(1, min(max_g2, -(-n // 1024)))
     per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)
-    return {"short_rows": short, "long_rows": long_, "G2": g2, "E": E}
+    return {"short_rows": short, "long_rows": long_, "G2": g2, "E": E,
+            "slices": auto_slices(a, long_)}
+
+
+def auto_slices(a, long_rows, bin_max=7936):
+    """tpl_runtime.cpp auto_slices + build_layout: the fewest of 1, 2, 4, 8 column slices
+    whose share of the vector (8 n bytes) fits 2 MiB, doubled while a (long row, slice)
+    piece holds more than bin_max entries."""
+    n = a.shape[0]
+    s = 1
+    while s < 8 and n * 8.0 / s > 2.0 * 1024 * 1024:
+        s *= 2
+
+    def widest(S):
+        w = 0
+        for r in long_rows:
+            c = a.indices[a.indptr[r]:a.indptr[r + 1]].astype(np.int64)
+            sl = np.searchsorted(np.array([n * k // S for k in range(1, S)], dtype=np.int64),
+                                 c, side="right")
+            w = max(w, int(np.bincount(sl, minlength=S).max()) if c.size else 0)
+        return w
+
+    while s < 8 and widest(s) > bin_max:
+        s *= 2
+    return s

@@ -80,6 +80,7 @@ def test_schedule_matches_rule(skewed):
     assert np.array_equal(sch["short_rows"], ref["short_rows"])
     assert np.array_equal(sch["long_rows"], ref["long_rows"])
     assert sch["G2"] == ref["G2"] and sch["E"] == ref["E"]
+    assert sch["slices"] == ref["slices"]
 
 
 @pytest.mark.parametrize("which", ["kkt5k", "skewed", "diag"])
@@ -104,6 +105,27 @@ def test_pass_one_bitwise(which, k, kkt5k, skewed):
     assert d.steps_taken == s == k
     assert d.b_norm == bn
     assert np.array_equal(d.alphas, al) and np.array_equal(d.betas, be)
+
+
+@pytest.mark.parametrize("slices", [1, 2, 4, 8])
+def test_slice_counts_bitwise(slices, kkt5k, skewed):
+    """Every long-row slice count (1: rows finished in place, no hand-off; 2-8: the
+    last-arriver hand-off) against the oracle in that order: SpMV, pass one, and the
+    two-pass x (pass two's grouped x updates)."""
+    for a, b in ((kkt5k.a, harness_b(kkt5k.a)), (skewed, std_rng_vector(skewed.shape[0]))):
+        op = HipCsrOp(a)
+        op.set_slices(slices)
+        assert op.schedule()["slices"] == slices
+        o = canon(op, a)
+        x = std_rng_vector(a.shape[0]) - 0.5
+        assert np.array_equal(op.apply(x), o.apply(x))
+        d = alg.lanczos_pass_one(op, b, 31)
+        al, be, st, bn, _ = o.pass_one(b, 31)
+        assert d.steps_taken == st
+        assert np.array_equal(d.alphas, al) and np.array_equal(d.betas, be)
+        assert np.array_equal(solvers.lanczos_two_pass(op, b, 31, ftk.EXP),
+                              o.lanczos_two_pass(b, 31, ftk.EXP))
+        op.close()
 
 
 def test_basis_regeneration_bitwise(skewed):

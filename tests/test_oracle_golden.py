@@ -116,7 +116,8 @@ def test_orthogonality_csv(func, scen):
 def test_unit_recurrence_alpha_beta():
     """src/algorithms/mod.rs:385-407: tridiag(-1,2,-1), v = e1 -> alpha = 2, beta = 1."""
     a = sp.diags([-np.ones(3), 2 * np.ones(4), -np.ones(3)], [-1, 0, 1]).tocsr()
-    for sched in (None, {"short_rows": [0, 1, 2, 3], "long_rows": [], "G2": 1, "E": 512}):
+    for sched in (None, {"short_rows": [0, 1, 2, 3], "long_rows": [], "G2": 1, "E": 512,
+                            "slices": 1}):
         op = oracle.Operator(a, sched)
         al, be, s, bn, _ = op.pass_one(np.array([1.0, 0, 0, 0]), 2)
         assert abs(al[0] - 2.0) < 1e-15 and abs(be[0] - 1.0) < 1e-15

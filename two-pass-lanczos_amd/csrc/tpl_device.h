@@ -11,29 +11,35 @@
 //     thread t owns positions C*c + t + 256q: every load is coalesced and no row
 //     pointer is chased. When every chunk has the same width W the chunk bases are
 //     computed, not loaded, and the kernel is specialised for W.
-//   * LONG rows are cut into kSlices column slices [floor(n*s/8), floor(n*(s+1)/8)).
-//     The (row, slice) pieces of slice s, long rows ascending, are packed whole into
-//     BINS of bin_cap entries (padding col = -1) with at most kBinSegs pieces each;
-//     every slice gets the same number M of bins. Bin m of slice s is workgroup
-//     8m + s of the slice part of the grid: under the round-robin dispatch of
-//     workgroups to XCDs all bins of a slice run on one XCD, whose L2 then only
-//     caches 1/8 of the gathered vector (speed only, never correctness). A bin's
-//     entries are read at computed addresses (thread t: entries t + 256u), the
-//     products are staged in LDS, and each piece is summed by 8 lanes. Every piece
-//     sum is published write-through into the row's slot (slots hold a sentinel
-//     while empty); after its store drains, the publisher reads the row's eight
-//     slots, and the one that sees all eight filled finalises the row (sums the
-//     slots, runs the epilogue, empties the slots). Nobody waits on anybody.
+//   * LONG rows are cut into S column slices [floor(n*s/S), floor(n*(s+1)/S)), S in
+//     {1, 2, 4, 8} (tpl_runtime.cpp auto_slices: the fewest whose share of the
+//     gathered vector fits half an L2). The (row, slice) pieces of slice s, long
+//     rows ascending, are packed whole into BINS of bin_cap entries (padding
+//     col = -1) with at most kBinSegs pieces each; every slice gets the same number
+//     M of bins. Bin m of slice s is workgroup S*m + s of the slice part of the
+//     grid: under the round-robin dispatch of workgroups to XCDs the bins of a slice
+//     run on 8/S XCDs, whose L2s then only cache 1/S of the gathered vector (speed
+//     only, never correctness). A bin's entries are read at computed addresses
+//     (thread t: entries t + 256u), the products are staged in LDS, and each piece
+//     is summed by 8 lanes (by a whole wave when longer than kBigPiece; those
+//     pieces lead the table). With S = 1 a piece is its whole row, finished in
+//     place. Otherwise every piece sum is published write-through into the row's
+//     slot (slots hold a sentinel while empty); after its store drains, the
+//     publisher reads the row's S slots, and the one that sees all S filled
+//     finalises the row (sums the slots, runs the epilogue, empties the slots).
+//     Nobody waits on anybody.
 //
 // Canonical reduction order (reproduced bit for bit by oracle/lanczos_oracle.c):
 //   * tree256(a[256])  : per 64-lane wave an xor butterfly (offsets 1,2,4,8,16,32,
 //                        a_l <- a_l + a_{l^off}), then (S0 + S1) + (S2 + S3).
 //   * partials(P[N])   : thread t: s_t = 0; s_t += P[t + 256q] (q ascending); tree256.
 //   * short row        : s = 0; s += round(a_k x_k), k ascending.
-//   * long row         : per slice s: lane g (0..7): p_g = 0; p_g += round(a_k x_k) for
-//                        the slice's entries k = g + 8q (q ascending); P_s = xor
-//                        butterfly of p over 8 lanes (offsets 1, 2, 4); y = 0; y += P_s,
-//                        s = 0..7.
+//   * long row         : per slice s, its L entries form a piece. L <= kBigPiece: lane
+//                        g (0..7): p_g = 0; p_g += round(a_k x_k) for the piece's
+//                        entries k = g + 8q (q ascending); P_s = xor butterfly of p over
+//                        8 lanes (offsets 1, 2, 4). L > kBigPiece: the same with 64
+//                        lanes (k = g + 64q) and the 64-lane butterfly of tree256.
+//                        y = 0; y += P_s, s = 0..S-1.
 //   * alpha partials   : Pa[c] (short chunk c): thread t: acc = fma(v, w, acc) over its
 //                        positions kChunkRows*c + t + 256q (q ascending), tree256;
 //                        Pa[n_chunks + r] (long row r) = round(v * w).
@@ -54,6 +60,9 @@ constexpr int kRowsPerThread = kChunkRows / kTPB;
 constexpr int kShortRowMax = 32;     // upper bound of the short-row threshold
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
 constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB table slots)
+// Pieces longer than this are summed by a whole wave (64 lanes), the others by 8 lanes;
+// the long pieces of a bin come first in its table (CsrDev::b_hdr holds their count).
+constexpr int kBigPiece = 64;
 #ifndef TPL_BIN_MIN
 #define TPL_BIN_MIN 2048
 #endif
@@ -69,6 +78,12 @@ constexpr double kBreakdownTol = 2.220446049250313080847263336181640625e-13; // 
 // One bin-table slot: piece start (offset in the bin), long-row index, global row.
 // Slot j < pieces describes piece j (its end is slot j+1's start); the slot after
 // the last piece holds the bin's fill with ri = row = -1, and so do all later slots.
+// x terms pass-two step j (1 .. last) applies (EpiPass2): the terms pending since the
+// previous flush, at every third step and at the last one.
+inline int p2_flush(int j, int last) {
+  return (j % 3 == 0 || j == last) ? j - ((j - 1) / 3) * 3 : 0;
+}
+
 struct BinSeg {
   int32_t start, ri, row, pad;
 };
@@ -88,7 +103,8 @@ struct CsrDev {
                             // offsets from b_cbase[bin] (0xFFFF padding) when b_col16
   const int32_t* b_cbase;   // per-bin column base (b_col16)
   const void* b_val;        // double, or int8_t when val_i8
-  const BinSeg* b_seg;      // n_bins x kTPB table slots
+  const BinSeg* b_seg;      // n_bins x kTPB table slots (pieces, then the end marker)
+  const int32_t* b_hdr;     // per bin: number of pieces | long pieces (first) << 16
   double* P;                // n_long x kSlices piece partials (sentinel when empty)
   int32_t val_i8;           // 1: every stored value is a small integer, kept as int8
   int32_t s_col16;          // 1: chunk columns as uint16 offsets
@@ -99,12 +115,12 @@ struct CsrDev {
   int32_t n_chunks;
   int32_t n_long;
   int32_t bin_cap;          // entries per bin (multiple of kTPB)
-  int32_t n_slice_blocks;   // kSlices * M; SpMV grid = n_chunks + n_slice_blocks
+  int32_t n_slice_blocks;   // n_slices * M; SpMV grid = n_chunks + n_slice_blocks
   int32_t G2;               // workgroups of the element-wise kernels == #norm partials
   int32_t NA;               // #alpha partials = n_chunks + n_long
   int32_t NA_r;             // #alpha partials the reducing kernel reads (NA, or more, see DevState)
   int32_t G2_r;             // #norm partials the reducing kernel reads (G2, or #ranks)
-  int32_t pad;
+  int32_t n_slices;         // column slices of the long rows (1, 2, 4 or 8 <= kSlices)
   int64_t n;
   int64_t E;                // elements per workgroup of the element-wise kernels
   // Replicated-long-row partition (tpl_runtime.cpp, "hybrid"): the SpMV stores each

@@ -42,6 +42,9 @@ namespace tpl {
 #ifndef TPL_STAMP
 #define TPL_STAMP 0
 #endif
+#ifndef TPL_PRE_LATE
+#define TPL_PRE_LATE 0  // experiment: chunk rows' own vector entries issued after the gathers
+#endif
 #if TPL_STAMP
 // Diagnostic builds only: per-workgroup s_memrealtime (100 MHz) marks of the most
 // recent SpMV-shaped launch — [0] start, [1] scale known, [2] products staged /
@@ -182,7 +185,12 @@ struct EpiPass1 {
   }
 };
 
-// pass two: w = (y - beta_{j-1} v_{j-1}) - alpha_j v_j; v_{j+1} = w / beta_j; x += y_{j+1} v_{j+1}
+// pass two: w = (y - beta_{j-1} v_{j-1}) - alpha_j v_j; v_{j+1} = w / beta_j; x += y_j v_{j+1}.
+// The x updates are applied in groups: a step with nflush = m adds the last m terms
+// (y_{j-2} v_{j-1}, y_{j-1} v_j, y_j v_{j+1}: all three are in registers) one after the
+// other, exactly as m separate steps would round them; nflush = 0 leaves x untouched.
+// The host flushes every third step and at the last one, so x is read and written once
+// per three steps instead of every step.
 struct Pre2 {
   double vc, vp, x;
 };
@@ -190,22 +198,47 @@ struct EpiPass2 {
   const double* v_cur;
   const double* v_prev; // == v_cur (never used) at j == 1 where v_0 = 0
   bool has_prev;
-  double beta_sub, alpha, invb, ycoef;
+  int nflush;           // 0..3 x terms applied by this step
+  double beta_sub, alpha, invb, ycoef, ycoef1, ycoef2;  // y[j], y[j-1], y[j-2]
   double* v_next;
   double* x;
   double* Vcol; // lanczos_pass_two_with_basis: column j of V'_k, else nullptr
-  __device__ __forceinline__ Pre2 pre(int i) const { return Pre2{v_cur[i], v_prev[i], x[i]}; }
+  __device__ __forceinline__ Pre2 pre(int i) const {
+    return Pre2{v_cur[i], v_prev[i], nflush ? x[i] : 0.0};
+  }
   __device__ __forceinline__ void apply(int i, double s, const Pre2& p, double&) const {
     const double vp = has_prev ? p.vp : 0.0;
     double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
     v_next[i] = vn;
-    x[i] = p.x + ycoef * vn;
+    if (nflush) {
+      double xv = p.x;
+      if (nflush >= 3) xv = xv + ycoef2 * p.vp;
+      if (nflush >= 2) xv = xv + ycoef1 * p.vc;
+      x[i] = xv + ycoef * vn;
+    }
     if (Vcol) Vcol[i] = vn;
   }
   __device__ __forceinline__ void long_alpha(int, double) const {}
 };
+__device__ __forceinline__ void p2_epi_init(EpiPass2& epi, const DevState& S, const double* v_cur,
+                                            const double* v_prev, double* v_next, double* x,
+                                            double* Vcol, int j, int nflush) {
+  epi.v_cur = v_cur;
+  epi.v_prev = (j >= 2) ? v_prev : v_cur;
+  epi.has_prev = j >= 2;
+  epi.nflush = nflush;
+  epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
+  epi.alpha = S.alphas[j - 1];
+  epi.invb = 1.0 / S.betas[j - 1];
+  epi.ycoef = S.y[j];
+  epi.ycoef1 = nflush >= 2 ? S.y[j - 1] : 0.0;
+  epi.ycoef2 = nflush >= 3 ? S.y[j - 2] : 0.0;
+  epi.v_next = v_next;
+  epi.x = x;
+  epi.Vcol = Vcol;
+}
 
 // keep() for a row's epilogue inputs (used only for live rows / finalising threads)
 __device__ __forceinline__ void keep_pre(PreNone&) {}
@@ -259,8 +292,8 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
     const int pc = clampi(p, A.n_short - 1);
     row[q] = A.s_identity ? pc : A.srows[pc];
   }
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
+  // Issue order = arrival order: the entries first (the gathers wait on them), then
+  // the row's own vector entries (needed only by the epilogue), then the gathers.
   int c[kRowsPerThread][W];
   double a[kRowsPerThread][W], xv[kRowsPerThread][W];
 #pragma unroll
@@ -271,10 +304,18 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
       c[q][k] = col_at<C16>(A.s_col, e, cbase);
       a[q][k] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.s_val, e);
     }
+#if !TPL_PRE_LATE
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
+#endif
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q)
 #pragma unroll
     for (int k = 0; k < W; ++k) xv[q][k] = xsrc[c[q][k] < 0 ? 0 : c[q][k]];
+#if TPL_PRE_LATE
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
+#endif
   const Scale sc = scale_of();
   TPL_MARK(1);
   if (!sc.ok) return false; // stopped / breakdown (uniform)
@@ -368,17 +409,20 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
 // Bin m of slice s. Thread t loads entries t + 256u of the bin (coalesced, at
 // computed addresses) and its bin-table slot; the products go to LDS; each piece is
 // then summed by one wave (lane-strided + butterfly) and handed back to thread j,
-// which owns piece j and publishes it; whoever completes a row's eight finalises it.
+// which owns piece j and publishes it; whoever completes a row's S slices finalises it
+// (S = 1: the piece is the row, finished in place).
 // lds: bin_cap doubles of products, kTPB ints of piece starts, kTPB piece sums.
 template <int V8, int C16, class Epi, class ScaleFn>
 __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                          const double* __restrict__ xsrc, ScaleFn scale_of,
                                          const Epi& epi, double* lds) {
   const int t = threadIdx.x;
-  const int bin = m * kSlices + s;
-  const BinSeg sg = A.b_seg[bin * kTPB + t];
+  const int bin = __builtin_amdgcn_readfirstlane(m * A.n_slices + s);  // scalar loads below
   const int base = bin * A.bin_cap;
   const int cbase = C16 ? A.b_cbase[bin] : 0;
+  const int hdr = A.b_hdr[bin];
+  // Issue order: the entries first (the gathers wait on them), then the bin table
+  // (its slot index waits on the header).
   int c[kBinBatch];
   double a[kBinBatch], xv[kBinBatch];
 #pragma unroll
@@ -386,6 +430,10 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
     c[u] = col_at<C16>(A.b_col, base + u * kTPB + t, cbase);
     a[u] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.b_val, base + u * kTPB + t);
   }
+  __builtin_amdgcn_sched_barrier(0);
+  // only the slots up to the end marker are read (threads past it re-read the marker)
+  const int npieces = hdr & 0xFFFF, nbig = hdr >> 16;
+  const BinSeg sg = A.b_seg[bin * kTPB + (t < npieces ? t : npieces)];
 #pragma unroll
   for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
   // the finalising thread's own row entries travel with the gathers
@@ -414,13 +462,32 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   int* starts = reinterpret_cast<int*>(lds + A.bin_cap);
   double* psum = lds + A.bin_cap + kTPB / 2;  // kTPB doubles after the starts
   starts[t] = sg.ri < 0 ? -1 - sg.start : sg.start;  // < 0: no piece (value encodes the fill)
-  const int npieces = __syncthreads_count(sg.ri >= 0);  // pieces are a prefix of the table
+  __syncthreads();
   TPL_MARK(2);
-  // Piece sums, 32 pieces per pass: the 8-lane group t >> 3 takes piece j0 + (t >> 3);
-  // its lane g sums the piece's entries g + 8q, then a butterfly over the 8 lanes
-  // (canonical long-row order).
+  // Piece sums (canonical long-row order). A piece longer than kBigPiece takes a whole
+  // wave: lane l sums its entries l + 64q, then the wave butterfly. Those pieces come
+  // first in the table (nbig of them), one wave each in turn.
+  const int lane = t & 63;
+  if (!(TPL_ABLATE & 4)) {
+    for (int j = t >> 6; j < nbig; j += kTPB / 64) {
+      const int st = starts[j], nx = starts[j + 1];
+      const int en = nx >= 0 ? nx : -1 - nx;
+      double acc = 0.0;
+      for (int k0 = st + lane; k0 < en; k0 += 512) {  // 8 reads in flight, then the adds
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 64 * u < en ? k0 + 64 * u : k0];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = k0 + 64 * u < en ? acc + v[u] : acc;
+      }
+      acc = wave_sum(acc);
+      if (lane == 0) psum[j] = acc;
+    }
+  }
+  // The other pieces, 32 per pass: the 8-lane group t >> 3 takes one; its lane g sums
+  // the piece's entries g + 8q, then a butterfly over the 8 lanes.
   const int g8 = t & 7;
-  for (int j0 = 0; j0 < npieces; j0 += kTPB / 8) {
+  for (int j0 = nbig; j0 < npieces; j0 += kTPB / 8) {
     const int j = j0 + (t >> 3);
     const int jc = j < kTPB - 2 ? j : kTPB - 2;
     const int st = starts[jc], nx = starts[jc + 1];
@@ -444,8 +511,20 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   TPL_MARK(3);
   if (sg.ri < 0) return; // no piece for this thread
   const double p = psum[t];
+  const int ns = A.n_slices;
+  if (ns == 1) {  // the piece is the whole row: no hand-off
+    const double y = 0.0 + p;
+    if (A.long_defer) {
+      A.ypart[sg.ri] = y;
+      return;
+    }
+    double acc = 0.0;
+    epi.apply(sg.row, y, pre, acc);
+    epi.long_alpha(sg.ri, acc);
+    return;
+  }
   // Hand-off, data-tagged: publish the piece sum write-through, drain, then read the
-  // row's eight slots. The publisher whose store completed last sees all eight, so
+  // row's S slots. The publisher whose store completed last sees all S, so
   // some thread always finalises; a tie finalises twice, writing identical bits
   // (every input — the slots, the row's vector entries loaded before publishing — is
   // the same). No thread ever waits on another: nothing depends on dispatch order.
@@ -456,18 +535,20 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   TPL_MARK(4);
   unsigned long long v[kSlices];
 #pragma unroll
-  for (int k = 0; k < kSlices; ++k)
-    v[k] = __hip_atomic_load(slots + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < kSlices; ++k)  // slots past the slice count: re-read slot 0
+    v[k] = __hip_atomic_load(slots + (k < ns ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   bool all = true;
 #pragma unroll
   for (int k = 0; k < kSlices; ++k) all = all && v[k] != kSliceSentinel;
   if (!all) return;
 #pragma unroll
   for (int k = 0; k < kSlices; ++k)  // empty again for the next launch
-    __hip_atomic_store(slots + k, kSliceSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (k < ns)
+      __hip_atomic_store(slots + k, kSliceSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double y = 0.0;
 #pragma unroll
-  for (int k = 0; k < kSlices; ++k) y = y + __longlong_as_double((long long)v[k]);
+  for (int k = 0; k < kSlices; ++k)
+    if (k < ns) y = y + __longlong_as_double((long long)v[k]);
   if (A.long_defer) {  // partitioned: this rank's part of the row; finished after the exchange
     A.ypart[sg.ri] = y;
     return;
@@ -496,7 +577,7 @@ __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __
   if (TPL_CHUNKS_FIRST) b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
   if (b < A.n_slice_blocks) {
     if (!(TPL_ABLATE & 1))
-      long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / kSlices, b % kSlices, xsrc, scale_of, epi, lds);
+      long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / A.n_slices, b % A.n_slices, xsrc, scale_of, epi, lds);
     return -1;
   }
   const int chunk = b - A.n_slice_blocks;
@@ -621,12 +702,19 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   const int64_t beg = (int64_t)blockIdx.x * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
   const double normj = S.norms[j - 1];
-  // this thread's first pair issued before alpha is known
+  // All of this thread's pairs (up to kAxPairs) are loaded before alpha is known, at
+  // clamped addresses (vectors are padded to 64 doubles, so a pair starting below
+  // `end` is always readable); the loads are unconditional so none is sunk behind the
+  // reduction.
+  constexpr int kAxPairs = 4;
   const int64_t i00 = beg + 2 * threadIdx.x;
-  double2 w0 = make_double2(0.0, 0.0), rc0 = make_double2(0.0, 0.0);
-  if (j < k && i00 + 1 < end) {
-    w0 = *reinterpret_cast<const double2*>(W + i00);
-    rc0 = *reinterpret_cast<const double2*>(r_cur + i00);
+  double2 w0[kAxPairs], rc0[kAxPairs];
+#pragma unroll
+  for (int q = 0; q < kAxPairs; ++q) {
+    const int64_t i0 = i00 + (int64_t)q * 2 * kTPB;
+    const int64_t ic = i0 < end ? i0 : beg;
+    w0[q] = *reinterpret_cast<const double2*>(W + ic);
+    rc0[q] = *reinterpret_cast<const double2*>(r_cur + ic);
   }
   if (stop) return;
   const double alpha = finish_partials(S.Pa_r, A.NA_r, pr, red);
@@ -637,28 +725,26 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   if (j == k) return; // beta_k is never used (src/algorithms/lanczos_two_pass.rs:252-254)
   const double invN = 1.0 / normj;
   double acc = 0.0;
-  for (int64_t i0 = i00; i0 < end; i0 += 2 * kTPB) {
+  auto step = [&](int64_t i0, double2 w, double2 rc) {
+    double2 r;
+    r.x = w.x - alpha * (rc.x * invN);
+    r.y = w.y - alpha * (rc.y * invN);
     if (i0 + 1 < end) {
-      double2 w, rc;
-      if (i0 == i00) {
-        w = w0;
-        rc = rc0;
-      } else {
-        w = *reinterpret_cast<const double2*>(W + i0);
-        rc = *reinterpret_cast<const double2*>(r_cur + i0);
-      }
-      double2 r;
-      r.x = w.x - alpha * (rc.x * invN);
-      r.y = w.y - alpha * (rc.y * invN);
       *reinterpret_cast<double2*>(r_next + i0) = r;
-      acc = i0 < A.norm_n ? fma(r.x, r.x, acc) : acc;
-      acc = i0 + 1 < A.norm_n ? fma(r.y, r.y, acc) : acc;
     } else {
-      const double r = W[i0] - alpha * (r_cur[i0] * invN);
-      r_next[i0] = r;
-      acc = i0 < A.norm_n ? fma(r, r, acc) : acc;
+      r_next[i0] = r.x;
     }
+    acc = i0 < A.norm_n ? fma(r.x, r.x, acc) : acc;
+    acc = i0 + 1 < end && i0 + 1 < A.norm_n ? fma(r.y, r.y, acc) : acc;
+  };
+#pragma unroll
+  for (int q = 0; q < kAxPairs; ++q) {
+    const int64_t i0 = i00 + (int64_t)q * 2 * kTPB;
+    if (i0 < end) step(i0, w0[q], rc0[q]);
   }
+  for (int64_t i0 = i00 + (int64_t)kAxPairs * 2 * kTPB; i0 < end; i0 += 2 * kTPB) // E > 2048
+    step(i0, *reinterpret_cast<const double2*>(W + i0),
+         *reinterpret_cast<const double2*>(r_cur + i0));
   const double p = block_sum(acc, red);
   if (threadIdx.x == 0) S.Pb[blockIdx.x] = p;
 }
@@ -688,19 +774,11 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, 
                                                   const double* __restrict__ v_prev,
                                                   double* __restrict__ v_next,
                                                   double* __restrict__ x,
-                                                  double* __restrict__ Vcol, int j) {
+                                                  double* __restrict__ Vcol, int j,
+                                                  int nflush) {
   extern __shared__ double lds[];
   EpiPass2 epi;
-  epi.v_cur = v_cur;
-  epi.v_prev = (j >= 2) ? v_prev : v_cur;
-  epi.has_prev = j >= 2;
-  epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
-  epi.alpha = S.alphas[j - 1];
-  epi.invb = 1.0 / S.betas[j - 1];
-  epi.ycoef = S.y[j];
-  epi.v_next = v_next;
-  epi.x = x;
-  epi.Vcol = Vcol;
+  p2_epi_init(epi, S, v_cur, v_prev, v_next, x, Vcol, j, nflush);
   double acc = 0.0;
   spmv_block<F>(A, xsrc, UnitScale{}, epi, acc, lds);
 }
@@ -762,18 +840,10 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p2(CsrDev A, DevState S,
                                                       const double* __restrict__ v_prev,
                                                       double* __restrict__ v_next,
                                                       double* __restrict__ x,
-                                                      double* __restrict__ Vcol, int j) {
+                                                      double* __restrict__ Vcol, int j,
+                                                      int nflush) {
   EpiPass2 epi;
-  epi.v_cur = v_cur;
-  epi.v_prev = (j >= 2) ? v_prev : v_cur;
-  epi.has_prev = j >= 2;
-  epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
-  epi.alpha = S.alphas[j - 1];
-  epi.invb = 1.0 / S.betas[j - 1];
-  epi.ycoef = S.y[j];
-  epi.v_next = v_next;
-  epi.x = x;
-  epi.Vcol = Vcol;
+  p2_epi_init(epi, S, v_cur, v_prev, v_next, x, Vcol, j, nflush);
   long_epi_rows(A, yall, R, epi);
 }
 
@@ -933,9 +1003,9 @@ hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, do
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   hipStream_t s) {
+                   int nflush, hipStream_t s) {
   if (spmv_grid(A) > 0)
-    TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j);
+    TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j, nflush);
   return hipGetLastError();
 }
 int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kLongEpiRows; }
@@ -954,10 +1024,10 @@ hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hip
 }
 hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, int R,
                        const double* v_cur, const double* v_prev, double* v_next, double* x,
-                       double* Vcol, int j, hipStream_t s) {
+                       double* Vcol, int j, int nflush, hipStream_t s) {
   if (A.n_long > 0)
     hipLaunchKernelGGL(k_long_epi_p2, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A, S, yall, R,
-                       v_cur, v_prev, v_next, x, Vcol, j);
+                       v_cur, v_prev, v_next, x, Vcol, j, nflush);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,

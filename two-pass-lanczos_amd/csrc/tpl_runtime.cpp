@@ -35,9 +35,10 @@ hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const do
                    double* r_next, int j, int k, hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, hipStream_t s);
+// nflush: x terms the step applies (tpl::p2_flush: every third step and the last)
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   hipStream_t s);
+                   int nflush, hipStream_t s);
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
                       hipStream_t s);
 hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
@@ -45,7 +46,7 @@ hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, i
                        double* Pa_long, int j, hipStream_t s);
 hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, int R,
                        const double* v_cur, const double* v_prev, double* v_next, double* x,
-                       double* Vcol, int j, hipStream_t s);
+                       double* Vcol, int j, int nflush, hipStream_t s);
 hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hipStream_t s);
 hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
                       int64_t E, hipStream_t s);
@@ -107,7 +108,18 @@ struct SchedParams {
   int64_t long_from = -1;           // >= 0: rows [long_from, n) are long, the rest short
   bool compress_values = true;      // int8 values when all values are small integers
   bool compress_cols = true;        // uint16 column offsets when the spans allow
+  int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
 };
+
+// Column slices of the long rows (auto rule): the fewest (1, 2, 4, 8) whose share of
+// the gathered vector fits in half an XCD's 4 MiB L2 — slice s runs on the XCDs
+// b % 8 == s (mod slices), so each L2 caches only its slice's columns — and, when a
+// (row, slice) piece would exceed one bin, more slices until every piece fits.
+static int auto_slices(int64_t n_cols) {
+  int s = 1;
+  while (s < kSlices && (double)n_cols * 8.0 / s > 2.0 * 1024.0 * 1024.0) s *= 2;
+  return s;
+}
 
 // Host copy of the SpMV layout (tpl_device.h).
 struct Layout {
@@ -125,7 +137,9 @@ struct Layout {
   bool s_col16 = false, b_col16 = false;  // uint16 column offsets from a per-chunk/bin base
   std::vector<uint16_t> s_col16v, b_col16v;
   std::vector<int32_t> s_cbase, b_cbase;
+  int32_t nslices = 1;              // column slices of the long rows
   std::vector<BinSeg> b_seg;        // n_bins x kTPB table slots
+  std::vector<int32_t> b_hdr;       // per bin: pieces | long pieces << 16
   int32_t bin_cap = kBinMin;
   int32_t M = 0;                    // bins per slice
   int G2 = 1;
@@ -216,33 +230,41 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
     for (int64_t c = 0; c < nchunks; ++c) uni = uni && L.c_width[c] == L.c_width[0];
     if (uni && L.c_width[0] > 0) L.s_width = L.c_width[0];
   }
-  // Long rows: piece (r, s) = entries of long row r with columns in slice s; the
-  // pieces of slice s, r ascending, are packed whole into bins (first fit in order).
+  // Long rows: piece (r, s) = entries of long row r with columns in slice s (columns
+  // [n_glob s / S, n_glob (s+1) / S)); the pieces of slice s, r ascending, are packed
+  // whole into bins (first fit in order).
   const size_t nl = L.lrows.size();
-  std::vector<int32_t> poff(nl * (kSlices + 1));
+  int S = sp.slices > 0 ? sp.slices : auto_slices(n_glob);
+  std::vector<int32_t> poff;
   int32_t widest = 0;
-  for (size_t r = 0; r < nl; ++r) {
-    const int32_t row = L.lrows[r];
-    int32_t q = rp[row];
-    for (int s = 0; s <= kSlices; ++s) {
-      const int64_t bound = n_glob * s / kSlices;
-      while (q < rp[row + 1] && col[q] < bound) ++q;
-      poff[r * (kSlices + 1) + s] = (s == kSlices) ? rp[row + 1] : q;
-      if (s > 0)
-        widest = std::max(widest, poff[r * (kSlices + 1) + s] - poff[r * (kSlices + 1) + s - 1]);
+  auto cut = [&](int ns) {
+    poff.assign(nl * (ns + 1), 0);
+    widest = 0;
+    for (size_t r = 0; r < nl; ++r) {
+      const int32_t row = L.lrows[r];
+      int32_t q = rp[row];
+      for (int s = 0; s <= ns; ++s) {
+        const int64_t bound = n_glob * s / ns;
+        while (q < rp[row + 1] && col[q] < bound) ++q;
+        poff[r * (ns + 1) + s] = (s == ns) ? rp[row + 1] : q;
+        if (s > 0) widest = std::max(widest, poff[r * (ns + 1) + s] - poff[r * (ns + 1) + s - 1]);
+      }
     }
-  }
+  };
+  cut(S);
+  while (widest > kBinMax && sp.slices <= 0 && S < kSlices) cut(S *= 2);
   if (widest > kBinMax)
     fail(TPL_ERR_UNSUPPORTED, "a long row has " + std::to_string(widest) +
-                                  " nonzeros in one of its 8 column slices (limit " +
-                                  std::to_string(kBinMax) + ")");
+                                  " nonzeros in one of its " + std::to_string(S) +
+                                  " column slices (limit " + std::to_string(kBinMax) + ")");
+  L.nslices = S;
   L.bin_cap = std::max<int32_t>(kBinMin, ((widest + kTPB - 1) / kTPB) * kTPB);
   L.bin_cap = ((L.bin_cap + kBinMin - 1) / kBinMin) * kBinMin;  // whole load batches
-  std::vector<std::vector<std::pair<int32_t, int32_t>>> bins[kSlices]; // (r, fill-at-start)
-  std::vector<int32_t> fill[kSlices];
-  for (int s = 0; s < kSlices && nl > 0; ++s) {
+  std::vector<std::vector<std::vector<std::pair<int32_t, int32_t>>>> bins(S); // (r, fill-at-start)
+  std::vector<std::vector<int32_t>> fill(S);
+  for (int s = 0; s < S && nl > 0; ++s) {
     for (size_t r = 0; r < nl; ++r) {
-      const int32_t cnt = poff[r * (kSlices + 1) + s + 1] - poff[r * (kSlices + 1) + s];
+      const int32_t cnt = poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
       if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
           (int)bins[s].back().size() == kBinSegs) {
         bins[s].emplace_back();
@@ -253,20 +275,34 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
     }
   }
   L.M = 0;
-  for (int s = 0; s < kSlices; ++s) L.M = std::max<int32_t>(L.M, (int32_t)bins[s].size());
-  const size_t nbins = (size_t)kSlices * L.M;
+  for (int s = 0; s < S; ++s) L.M = std::max<int32_t>(L.M, (int32_t)bins[s].size());
+  const size_t nbins = (size_t)S * L.M;
   L.b_col.assign(std::max<size_t>(nbins * L.bin_cap, 1), -1);
   L.b_val.assign(std::max<size_t>(nbins * L.bin_cap, 1), 0.0);
   L.b_seg.assign(std::max<size_t>(nbins * kTPB, 1), BinSeg{0, -1, -1, 0});
-  for (int s = 0; s < kSlices; ++s)
+  L.b_hdr.assign(std::max<size_t>(nbins, 1), 0);
+  for (int s = 0; s < S; ++s)
     for (int32_t m = 0; m < L.M; ++m) {
-      const size_t bin = (size_t)m * kSlices + s;
+      const size_t bin = (size_t)m * S + s;
       int32_t f = 0;
       if (m < (int32_t)bins[s].size()) {
-        const auto& pieces = bins[s][m];
+        // the pieces longer than kBigPiece first (summed a wave each), then the rest;
+        // entries are laid out in that table order
+        auto pieces = bins[s][m];
+        auto len = [&](int32_t r) {
+          return poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
+        };
+        std::stable_partition(pieces.begin(), pieces.end(),
+                              [&](const std::pair<int32_t, int32_t>& p) { return len(p.first) > kBigPiece; });
+        int32_t nbig = 0, at = 0;
+        for (auto& p : pieces) {
+          nbig += len(p.first) > kBigPiece;
+          p.second = at;
+          at += len(p.first);
+        }
         for (size_t j = 0; j < pieces.size(); ++j) {
           const int32_t r = pieces[j].first, start = pieces[j].second;
-          const int32_t q0 = poff[r * (kSlices + 1) + s], q1 = poff[r * (kSlices + 1) + s + 1];
+          const int32_t q0 = poff[r * (S + 1) + s], q1 = poff[r * (S + 1) + s + 1];
           L.b_seg[bin * kTPB + j] = BinSeg{start, r, L.lrows[r], 0};
           for (int32_t q = q0; q < q1; ++q) {
             L.b_col[bin * L.bin_cap + start + (q - q0)] = cmap(col[q]);
@@ -276,6 +312,7 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
         f = fill[s][m];
         for (size_t j = pieces.size(); j < (size_t)kTPB; ++j)
           L.b_seg[bin * kTPB + j] = BinSeg{f, -1, -1, 0};
+        L.b_hdr[bin] = (int32_t)pieces.size() | nbig << 16;
       }
     }
   // Value compression: when every stored value (padding included) is an integer in
@@ -318,7 +355,7 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
   // chunks have a uniform stride only when the widths are uniform (else per-chunk bases)
   if (L.s_width > 0)
     L.s_col16 = compress_cols(L.s_col, nchunks, (int64_t)L.s_width * kChunkRows, L.s_col16v, L.s_cbase);
-  L.b_col16 = compress_cols(L.b_col, (int64_t)kSlices * L.M, L.bin_cap, L.b_col16v, L.b_cbase);
+  L.b_col16 = compress_cols(L.b_col, (int64_t)L.nslices * L.M, L.bin_cap, L.b_col16v, L.b_cbase);
   if (L.s_col16) std::vector<int32_t>().swap(L.s_col);
   if (L.b_col16) std::vector<int32_t>().swap(L.b_col);
   const int64_t g2 = (n + 1023) / 1024;
@@ -376,6 +413,7 @@ struct tpl_op_s {
   Layout lay;
   void* d_bcol = nullptr;
   int32_t* d_bcbase = nullptr;
+  int32_t* d_bhdr = nullptr;
   int32_t* d_scbase = nullptr;
   void* d_bval = nullptr;
   BinSeg* d_bseg = nullptr;
@@ -438,6 +476,7 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.b_col = op->d_bcol;
   A.b_val = op->d_bval;
   A.b_seg = op->d_bseg;
+  A.b_hdr = op->d_bhdr;
   A.P = op->d_P;
   A.s_width = L.s_width;
   A.s_identity = L.s_identity;
@@ -445,7 +484,8 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.n_chunks = (int32_t)L.c_base.size();
   A.n_long = (int32_t)L.lrows.size();
   A.bin_cap = L.bin_cap;
-  A.n_slice_blocks = kSlices * L.M;
+  A.n_slices = L.nslices;
+  A.n_slice_blocks = L.nslices * L.M;
   A.G2 = L.G2;
   A.NA = A.n_chunks + A.n_long;
   A.NA_r = op->dist ? op->dist->nranks + (op->hybrid ? long_epi_blocks(op) : 0) : A.NA;
@@ -454,7 +494,6 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * L.lrows.size() : nullptr;
   A.pad2 = 0;
   A.norm_n = op->hybrid && op->dist->rank != 0 ? op->ns_local : op->n;
-  A.pad = 0;
   A.n = op->n;
   A.E = L.E;
   return A;
@@ -507,6 +546,7 @@ void rebuild_schedule(tpl_op_s* op) {
   else
     upload(reinterpret_cast<double**>(&op->d_bval), L.b_val);
   upload(&op->d_bseg, L.b_seg);
+  upload(&op->d_bhdr, L.b_hdr);
   // piece slots start empty (sentinel)
   std::vector<unsigned long long> empty(std::max<size_t>(L.lrows.size() * kSlices, 1),
                                         kSliceSentinel);
@@ -716,15 +756,16 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
   const CsrDev A = csr_dev(op);
   for (int j = 1; j < (int)steps; ++j) {
     double* Vcol = Vout ? Vout + (size_t)j * op->n : nullptr;
+    const int nflush = p2_flush(j, (int)steps - 1);
     HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
-                           Vcol, j, op->stream));
+                           Vcol, j, nflush, op->stream));
     if (op->hybrid) {
       const size_t nl = op->lay.lrows.size();
       if (nl) dist_allgather(op, op->d_yall, nl);
       HIPCHK(launch::long_epi_p2(A, op->S, op->d_yall, op->dist->nranks, op->V2[j % 3],
                                  j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3],
-                                 op->x, Vcol, j, op->stream));
+                                 op->x, Vcol, j, nflush, op->stream));
     } else if (op->dist && j + 1 < (int)steps) {
       dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
     }
@@ -1010,7 +1051,7 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipSetDevice(op->device);
     hipStreamSynchronize(op->stream);
     drop_graphs(op);
-    for (void* p : {(void*)op->d_bcol, (void*)op->d_bval, (void*)op->d_bseg, (void*)op->d_P,
+    for (void* p : {(void*)op->d_bcol, (void*)op->d_bval, (void*)op->d_bseg, (void*)op->d_bhdr, (void*)op->d_P,
                     (void*)op->d_bcbase, (void*)op->d_scbase,
                     (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval,
                     (void*)op->d_cbase, (void*)op->d_cwidth})
@@ -1253,6 +1294,25 @@ tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g
   });
 }
 
+tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices) {
+  return guarded([&] {
+    if (!op || !slices) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    *slices = op->lay.nslices;
+  });
+}
+
+tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    if (slices != 0 && slices != 1 && slices != 2 && slices != 4 && slices != 8)
+      fail(TPL_ERR_INVALID_ARGUMENT, "slices must be 0 (auto), 1, 2, 4 or 8");
+    set_device(op);
+    op->sp.slices = slices;
+    sync_checked(op);
+    rebuild_schedule(op);
+  });
+}
+
 tpl_status tpl_copy_to_host(void* dst, const void* src_device, size_t bytes) {
   return guarded([&] {
     if (bytes == 0) return;
@@ -1272,7 +1332,8 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
     case TPL_KERNEL_SPMV: return spmv;
     case TPL_KERNEL_PASS1_SPMV: return spmv + 8.0 * n;   // + r_{j-1} read (w is the y write)
     case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;         // w, r_j read; r_{j+1} written
-    case TPL_KERNEL_PASS2_SPMV: return spmv + 24.0 * n;  // + v_{j-1}, x read, x written
+    // + v_{j-1} read; x read and written once per three steps (grouped x updates)
+    case TPL_KERNEL_PASS2_SPMV: return spmv + 8.0 * n + 16.0 * n / 3.0;
     default: return 0.0;
   }
 }
@@ -1325,7 +1386,8 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
           break;
         case TPL_KERNEL_PASS2_SPMV:
           HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3], op->V2[(i + 1) % 3],
-                                 op->V2[i % 3], op->x, nullptr, 2, op->stream));
+                                 op->V2[i % 3], op->x, nullptr, 2, i % 3 == 2 ? 3 : 0,
+                                 op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }

@@ -122,8 +122,8 @@ class HipCsrOp:
 
     # -- schedule / measurement ------------------------------------------------
     def schedule(self):
-        """Device layout: dict(short_rows, long_rows, G2, E) — what the oracle needs to
-        reproduce the device reduction order."""
+        """Device layout: dict(short_rows, long_rows, G2, E, slices) — what the oracle
+        needs to reproduce the device reduction order."""
         ns, nl, g2, e = c_int32(), c_int32(), c_int32(), c_int64()
         check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e), None, None))
         sr = np.zeros(max(ns.value, 1), dtype=np.int32)
@@ -131,11 +131,17 @@ class HipCsrOp:
         check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e),
                                    sr.ctypes.data_as(POINTER(c_int32)),
                                    lr.ctypes.data_as(POINTER(c_int32))))
+        sl = c_int32()
+        check(_lib.tpl_op_slices(self._op, byref(sl)))
         return {"short_rows": sr[:ns.value].copy(), "long_rows": lr[:nl.value].copy(),
-                "G2": g2.value, "E": e.value}
+                "G2": g2.value, "E": e.value, "slices": sl.value}
 
     def set_schedule(self, short_row_max=0, max_g2=0):
         check(_lib.tpl_op_set_schedule(self._op, short_row_max, max_g2))
+
+    def set_slices(self, slices=0):
+        """Column slices of the long rows: 1, 2, 4, 8, or 0 for the auto rule."""
+        check(_lib.tpl_op_set_slices(self._op, slices))
 
     def profile_kernel(self, kernel: int, iters: int = 200):
         """(avg microseconds per launch, algorithmic bytes per launch) via HIP events."""
