@@ -7,7 +7,7 @@ mkdir -p ../../scripts/ablate
 for spec in "$@"; do
   A=${spec%%=*}; DEFS=${spec#*=}
   rm -rf build_ab$A && mkdir -p build_ab$A
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 $DEFS -c tpl_kernels.hip -o build_ab$A/k.o
+  for f in tpl_kernels tpl_push; do /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 $DEFS -c $f.hip -o build_ab$A/$f.o; done
   for f in tpl_runtime tpl_ftk tpl_loader; do /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off $DEFS -c $f.cpp -o build_ab$A/$f.o; done
   /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o ../../scripts/ablate/libtpl_amd_ab$A.so build_ab$A/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
   rm -rf build_ab$A

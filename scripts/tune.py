@@ -20,8 +20,9 @@ a = load_kkt_system(os.path.join(ROOT, "tests/golden/kkt", f"netgen-{arcs}-3.dmx
 n = a.shape[0]
 b = a @ np.full(n, 1 / np.sqrt(n))
 op = tpl_amd.HipCsrOp(a)
+op.set_slices(int(os.environ.get("SLICES", "0")))
 tpl_amd.lanczos_two_pass(op, b, 50, "inv")
-row = {"lib": os.path.basename(tpl_amd.LIB_PATH)}
+row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "slices": op.schedule()["slices"]}
 for kid, nm in [(0, "p1_spmv"), (1, "p1_axpy"), (2, "p2_spmv"), (3, "spmv")]:
     us, by = op.profile_kernel(kid, 300)
     row[nm] = round(us, 2)

@@ -72,15 +72,50 @@ def op5k(kkt5k):
     return HipCsrOp(kkt5k)
 
 
-def test_schedule_matches_rule(skewed):
-    op = HipCsrOp(skewed)
-    sch = op.schedule()
-    ref = canon_schedule(skewed)
-    assert len(sch["short_rows"]) > 0 and len(sch["long_rows"]) > 0
-    assert np.array_equal(sch["short_rows"], ref["short_rows"])
-    assert np.array_equal(sch["long_rows"], ref["long_rows"])
-    assert sch["G2"] == ref["G2"] and sch["E"] == ref["E"]
-    assert sch["slices"] == ref["slices"]
+@pytest.mark.parametrize("which", ["skewed", "kkt5k", "kkt50k"])
+def test_schedule_matches_rule(which, skewed, kkt5k, kkt50k):
+    a = {"skewed": skewed, "kkt5k": kkt5k.a, "kkt50k": kkt50k.a}[which]
+    op = HipCsrOp(a)
+    for push in (False, True):
+        op.set_push(push)
+        sch = op.schedule()
+        ref = canon_schedule(a, push=push)
+        assert len(sch["short_rows"]) > 0 and len(sch["long_rows"]) > 0
+        assert np.array_equal(sch["short_rows"], ref["short_rows"])
+        assert np.array_equal(sch["long_rows"], ref["long_rows"])
+        assert sch["G2"] == ref["G2"] and sch["E"] == ref["E"]
+        assert sch["slices"] == ref["slices"]
+        # pushed long rows (opt-in) exactly for the KKT operators (mirrored entries)
+        assert sch["push"] == ref["push"] == (push and which != "skewed")
+        assert sch["chunk_rows"] == ref["chunk_rows"]
+
+
+@pytest.mark.parametrize("push", [True, False])
+@pytest.mark.parametrize("which", ["kkt5k", "kkt50k"])
+def test_push_and_bins_layouts_bitwise(push, which, kkt5k, kkt50k):
+    """Both long-row layouts of a KKT operator against the oracle in that layout's
+    order: SpMV, pass one, pass two with its basis (== pass one's, bit for bit), x."""
+    a = {"kkt5k": kkt5k.a, "kkt50k": kkt50k.a}[which]
+    b = harness_b(a)
+    op = HipCsrOp(a)
+    op.set_push(push)
+    assert op.pushed == push
+    o = canon(op, a)
+    x = std_rng_vector(a.shape[0]) - 0.5
+    assert np.array_equal(op.apply(x), o.apply(x))
+    k = 60
+    out = alg.lanczos_standard(op, b, k)
+    al, be, st, bn, V = o.pass_one(b, k, store_basis=True)
+    d = out.decomposition
+    assert d.steps_taken == st and d.b_norm == bn
+    assert np.array_equal(d.alphas, al) and np.array_equal(d.betas, be)
+    assert np.array_equal(np.asarray(out.v_k), V)
+    y = ftk.EXP(d.alphas, d.betas) * d.b_norm
+    p2 = alg.lanczos_pass_two_with_basis(op, b, d, y)
+    assert np.array_equal(np.asarray(p2.v_k), V)      # P1: regenerated basis
+    xo, _ = o.pass_two(b, al, be, st, bn, y)
+    assert np.array_equal(np.asarray(p2.x_k), xo)
+    op.close()
 
 
 @pytest.mark.parametrize("which", ["kkt5k", "skewed", "diag"])

@@ -27,578 +27,9 @@
 // epilogue vectors) before its first wait. A short-row chunk costs two round trips
 // (entries -> gathers); a long-row bin the same two plus an LDS pass, and the
 // slice-7 bins one more (polling the other slices' partials).
-#include <hip/hip_runtime.h>
-#include "tpl_device.h"
-
-// Performance-ablation switches for experiments only (scripts/ablate.sh builds
-// separate libraries); production builds have TPL_ABLATE == 0. Bit 1: skip the
-// long-row bins; 2: skip the short chunks; 4: skip the bins' piece sums.
-#ifndef TPL_ABLATE
-#define TPL_ABLATE 0
-#endif
+#include "tpl_kcommon.h"
 
 namespace tpl {
-
-#ifndef TPL_STAMP
-#define TPL_STAMP 0
-#endif
-#ifndef TPL_PRE_LATE
-#define TPL_PRE_LATE 0  // experiment: chunk rows' own vector entries issued after the gathers
-#endif
-#if TPL_STAMP
-// Diagnostic builds only: per-workgroup s_memrealtime (100 MHz) marks of the most
-// recent SpMV-shaped launch — [0] start, [1] scale known, [2] products staged /
-// row sums done, [3] piece sums staged, [4] publish drained, [5] end — read back
-// by tpl_debug_stamps().
-constexpr int kMarks = 6;
-__device__ unsigned long long g_stamps[kMarks * 65536];
-#define TPL_MARK(k)                                                          \
-  do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x < 65536)                              \
-      g_stamps[kMarks * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#else
-#define TPL_MARK(k) do {} while (0)
-#endif
-
-// ---------------------------------------------------------------- reductions
-// 64-bit lane exchange through a DPP pattern (two 32-bit moves).
-template <int kCtrl>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)b, kCtrl, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), kCtrl, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ double swz_xor16_f64(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_ds_swizzle((int)b, 0x401F);  // bitmode: xor 16 within 32
-  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x401F);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)b, l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-// Sum over the 64 lanes of a wave (all lanes active), as the xor butterfly with
-// offsets 1, 2, 4, 8, 16, 32: lane l <- a_l + a_{l^h}. Once a stage is done every
-// group of 2h lanes holds one value, so any exchange pairing a group with its
-// partner group gives the same bits (IEEE addition is commutative); that lets the
-// stages run on DPP (quad_perm, half-row and row mirrors), one swizzle and a
-// readlane instead of LDS permutes. Every lane returns the same, order-fixed value.
-__device__ __forceinline__ double wave_sum(double v) {
-  v = v + dpp_f64<0xB1>(v);   // quad_perm [1,0,3,2]: xor 1
-  v = v + dpp_f64<0x4E>(v);   // quad_perm [2,3,0,1]: xor 2
-  v = v + dpp_f64<0x141>(v);  // row_half_mirror: partner quad in the 8-lane group
-  v = v + dpp_f64<0x140>(v);  // row_mirror: partner 8-lane group in the row
-  v = v + swz_xor16_f64(v);   // xor 16
-  return readlane_f64(v, 0) + readlane_f64(v, 32);
-}
-
-// Sum over each aligned group of 8 lanes (butterfly offsets 1, 2, 4), all on DPP.
-__device__ __forceinline__ double group8_sum(double v) {
-  v = v + dpp_f64<0xB1>(v);   // xor 1
-  v = v + dpp_f64<0x4E>(v);   // xor 2
-  v = v + dpp_f64<0x141>(v);  // partner quad in the 8-lane group
-  return v;
-}
-
-// tree256; every thread returns the block total. red: 4 doubles of LDS.
-__device__ __forceinline__ double block_sum(double v, double* red) {
-  v = wave_sum(v);
-  const int w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) red[w] = v;
-  __syncthreads();
-  const double r = (red[0] + red[1]) + (red[2] + red[3]);
-  __syncthreads();
-  return r;
-}
-
-// Issue the partial loads (independent) early ...
-template <int R>
-struct PartialRegs {
-  double v[R];
-};
-// (Every load below is unconditional with a clamped index and its result masked
-// afterwards: a load under a runtime condition makes hipcc branch around it and
-// drain vmcnt per element, serialising the round trips — guide §5 trap (c).)
-__device__ __forceinline__ int clampi(int i, int hi) { return i < hi ? i : hi; }
-template <int R>
-__device__ __forceinline__ void load_partials(const double* __restrict__ P, int N,
-                                              PartialRegs<R>& r) {
-#pragma unroll
-  for (int u = 0; u < R; ++u) r.v[u] = P[clampi(threadIdx.x + u * kTPB, N - 1)];
-}
-// ... and reduce them later in the canonical order (s = 0; s += P[t + 256q]).
-template <int R>
-__device__ __forceinline__ double finish_partials(const double* __restrict__ P, int N,
-                                                  const PartialRegs<R>& r, double* red) {
-  double s = 0.0;
-#pragma unroll
-  for (int u = 0; u < R; ++u)
-    if ((int)threadIdx.x + u * kTPB < N) s = s + r.v[u];
-  for (int i = threadIdx.x + R * kTPB; i < N; i += kTPB) s = s + P[i]; // N > 256 R (rare)
-  return block_sum(s, red);
-}
-
-// Pins a value as computed unconditionally: without it the compiler sinks the loads
-// feeding a product used under a select (padding entries) into a branch, where they
-// issue late behind an s_waitcnt vmcnt(0) and serialise the workgroup's round trips.
-__device__ __forceinline__ void keep(double& v) { asm volatile("" : "+v"(v)); }
-
-// ----------------------------------------------------------- epilogues
-// pre(i) loads the row's own vector entries (issued early); apply(i, s, pre, acc)
-// finishes the row given its SpMV sum s (acc: the thread's alpha accumulator).
-struct PreNone {};
-struct EpiSpmv {
-  double* y;
-  __device__ __forceinline__ PreNone pre(int) const { return {}; }
-  __device__ __forceinline__ void apply(int i, double s, const PreNone&, double&) const { y[i] = s; }
-  __device__ __forceinline__ void long_alpha(int, double) const {}
-};
-
-// pass one / standard: w = y - beta_{j-1} v_{j-1}; alpha partial += v_j . w
-struct Pre1 {
-  double rc, rp;
-};
-struct EpiPass1 {
-  const double* r_cur;  // r_j (v_j = r_j * invN_cur)
-  const double* r_prev; // r_{j-1}; == r_cur (never used) at j == 1 where v_0 = 0
-  bool has_prev;
-  double invN_cur, invN_prev, beta_sub;
-  double* W;
-  double* Vcol;         // standard variant: column j-1 of V_k, else nullptr
-  double* Pa_long;      // alpha partials of the long rows (Pa + n_chunks)
-  __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
-  // long row r: its alpha partial is the single rounded product v * w
-  __device__ __forceinline__ void long_alpha(int r, double acc) const { Pa_long[r] = acc; }
-  __device__ __forceinline__ void apply(int i, double s, const Pre1& p, double& acc) const {
-    const double v = p.rc * invN_cur;
-    const double vp = has_prev ? p.rp * invN_prev : 0.0;
-    const double w = s - beta_sub * vp;
-    W[i] = w;
-    if (Vcol) Vcol[i] = v;
-    acc = fma(v, w, acc);
-  }
-};
-
-// pass two: w = (y - beta_{j-1} v_{j-1}) - alpha_j v_j; v_{j+1} = w / beta_j; x += y_j v_{j+1}.
-// The x updates are applied in groups: a step with nflush = m adds the last m terms
-// (y_{j-2} v_{j-1}, y_{j-1} v_j, y_j v_{j+1}: all three are in registers) one after the
-// other, exactly as m separate steps would round them; nflush = 0 leaves x untouched.
-// The host flushes every third step and at the last one, so x is read and written once
-// per three steps instead of every step.
-struct Pre2 {
-  double vc, vp, x;
-};
-struct EpiPass2 {
-  const double* v_cur;
-  const double* v_prev; // == v_cur (never used) at j == 1 where v_0 = 0
-  bool has_prev;
-  int nflush;           // 0..3 x terms applied by this step
-  double beta_sub, alpha, invb, ycoef, ycoef1, ycoef2;  // y[j], y[j-1], y[j-2]
-  double* v_next;
-  double* x;
-  double* Vcol; // lanczos_pass_two_with_basis: column j of V'_k, else nullptr
-  __device__ __forceinline__ Pre2 pre(int i) const {
-    return Pre2{v_cur[i], v_prev[i], nflush ? x[i] : 0.0};
-  }
-  __device__ __forceinline__ void apply(int i, double s, const Pre2& p, double&) const {
-    const double vp = has_prev ? p.vp : 0.0;
-    double w = s - beta_sub * vp;
-    w = w - alpha * p.vc;
-    const double vn = w * invb;
-    v_next[i] = vn;
-    if (nflush) {
-      double xv = p.x;
-      if (nflush >= 3) xv = xv + ycoef2 * p.vp;
-      if (nflush >= 2) xv = xv + ycoef1 * p.vc;
-      x[i] = xv + ycoef * vn;
-    }
-    if (Vcol) Vcol[i] = vn;
-  }
-  __device__ __forceinline__ void long_alpha(int, double) const {}
-};
-__device__ __forceinline__ void p2_epi_init(EpiPass2& epi, const DevState& S, const double* v_cur,
-                                            const double* v_prev, double* v_next, double* x,
-                                            double* Vcol, int j, int nflush) {
-  epi.v_cur = v_cur;
-  epi.v_prev = (j >= 2) ? v_prev : v_cur;
-  epi.has_prev = j >= 2;
-  epi.nflush = nflush;
-  epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
-  epi.alpha = S.alphas[j - 1];
-  epi.invb = 1.0 / S.betas[j - 1];
-  epi.ycoef = S.y[j];
-  epi.ycoef1 = nflush >= 2 ? S.y[j - 1] : 0.0;
-  epi.ycoef2 = nflush >= 3 ? S.y[j - 2] : 0.0;
-  epi.v_next = v_next;
-  epi.x = x;
-  epi.Vcol = Vcol;
-}
-
-// keep() for a row's epilogue inputs (used only for live rows / finalising threads)
-__device__ __forceinline__ void keep_pre(PreNone&) {}
-__device__ __forceinline__ void keep_pre(Pre1& p) { keep(p.rc); keep(p.rp); }
-__device__ __forceinline__ void keep_pre(Pre2& p) { keep(p.vc); keep(p.vp); keep(p.x); }
-
-// Result of a workgroup's prologue: the gather scale, or "stop" (uniform across the grid).
-struct Scale {
-  double s;
-  bool ok;
-};
-struct UnitScale {
-  __device__ __forceinline__ Scale operator()() const { return Scale{1.0, true}; }
-};
-
-// Matrix values: fp64, or int8 when every value is a small integer (V8 = 1; the
-// conversion to double is exact, so products and sums are bit-identical).
-template <int V8>
-__device__ __forceinline__ double val_at(const void* p, int i) {
-  if (V8) return (double)reinterpret_cast<const int8_t*>(p)[i];
-  return reinterpret_cast<const double*>(p)[i];
-}
-
-// Column indices: int32 (padding -1), or — C16 — uint16 offsets from a per-chunk /
-// per-bin base (padding 0xFFFF) when every chunk / bin spans fewer than 65535 columns.
-template <int C16>
-__device__ __forceinline__ int col_at(const void* p, int i, int base) {
-  if (C16) {
-    const int off = reinterpret_cast<const uint16_t*>(p)[i];
-    return off == 0xFFFF ? -1 : base + off;
-  }
-  return reinterpret_cast<const int32_t*>(p)[i];
-}
-
-// ------------------------------------------------------ short rows (sliced ELL)
-// Chunk with a compile-time width W (entries loaded unconditionally: the sliced-ELL
-// storage is allocated for whole chunks, padding has col = -1).
-template <int W, int V8, int C16, class Epi, class ScaleFn>
-__device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int base,
-                                              const double* __restrict__ xsrc, ScaleFn scale_of,
-                                              const Epi& epi, double& acc) {
-  const int t = threadIdx.x;
-  const int cbase = C16 ? A.s_cbase[chunk] : 0;
-  int row[kRowsPerThread];
-  bool live[kRowsPerThread];
-  decltype(epi.pre(0)) pre[kRowsPerThread];
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    const int p = chunk * kChunkRows + q * kTPB + t;
-    live[q] = p < A.n_short;
-    const int pc = clampi(p, A.n_short - 1);
-    row[q] = A.s_identity ? pc : A.srows[pc];
-  }
-  // Issue order = arrival order: the entries first (the gathers wait on them), then
-  // the row's own vector entries (needed only by the epilogue), then the gathers.
-  int c[kRowsPerThread][W];
-  double a[kRowsPerThread][W], xv[kRowsPerThread][W];
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q)
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int e = base + k * kChunkRows + q * kTPB + t;
-      c[q][k] = col_at<C16>(A.s_col, e, cbase);
-      a[q][k] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.s_val, e);
-    }
-#if !TPL_PRE_LATE
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
-#endif
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q)
-#pragma unroll
-    for (int k = 0; k < W; ++k) xv[q][k] = xsrc[c[q][k] < 0 ? 0 : c[q][k]];
-#if TPL_PRE_LATE
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
-#endif
-  const Scale sc = scale_of();
-  TPL_MARK(1);
-  if (!sc.ok) return false; // stopped / breakdown (uniform)
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) keep_pre(pre[q]);
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    double sum = 0.0;
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-      double prod = a[q][k] * (xv[q][k] * sc.s);
-      keep(prod);
-      sum = c[q][k] >= 0 ? sum + prod : sum;
-    }
-    if (live[q]) epi.apply(row[q], sum, pre[q], acc);
-  }
-  TPL_MARK(2);
-  return true;
-}
-
-// Any width (rare: chunks wider than 4). One row position at a time, entries in
-// batches of 8 with every load of a batch in flight; kept lean in registers, since a
-// kernel's VGPR budget is the maximum over all of its paths.
-template <int V8, int C16, class Epi, class ScaleFn>
-__device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int base, int W,
-                                                const double* __restrict__ xsrc, ScaleFn scale_of,
-                                                const Epi& epi, double& acc) {
-  const int t = threadIdx.x;
-  const int cbase = C16 ? A.s_cbase[chunk] : 0;
-  const Scale sc = scale_of();
-  if (!sc.ok) return false;
-#pragma unroll 1
-  for (int q = 0; q < kRowsPerThread; ++q) {
-    const int p = chunk * kChunkRows + q * kTPB + t;
-    const bool live = p < A.n_short;
-    const int pc = clampi(p, A.n_short - 1);
-    const int row = A.s_identity ? pc : A.srows[pc];
-    auto pre = epi.pre(row);
-    double s = 0.0;
-#pragma unroll 1
-    for (int k0 = 0; k0 < W; k0 += 8) {
-      int c[8];
-      double a[8], xv[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = base + clampi(k0 + u, W - 1) * kChunkRows + q * kTPB + t;
-        c[u] = col_at<C16>(A.s_col, e, cbase);
-        a[u] = val_at<V8>(A.s_val, e);
-      }
-#pragma unroll
-      for (int u = 0; u < 8; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        double prod = a[u] * (xv[u] * sc.s);
-        keep(prod);
-        s = (c[u] >= 0 && k0 + u < W) ? s + prod : s;
-      }
-    }
-    keep_pre(pre);
-    if (live) epi.apply(row, s, pre, acc);
-  }
-  return true;
-}
-
-// CW > 0: the kernel was specialised for a uniform chunk width CW (tpl::launch picks
-// it from A.s_width); CW == 0: generic, any per-chunk width.
-template <int CW, int V8, int C16, class Epi, class ScaleFn>
-__device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
-                                            const double* __restrict__ xsrc, ScaleFn scale_of,
-                                            const Epi& epi, double& acc) {
-  if (CW > 0)
-    return short_chunk_w<CW, V8, C16>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
-  int W, base;
-  if (A.s_width > 0) {
-    W = A.s_width;
-    base = chunk * kChunkRows * W;
-  } else {
-    W = A.c_width[chunk];
-    base = A.c_base[chunk];
-  }
-  switch (W) {
-    case 1: return short_chunk_w<1, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 2: return short_chunk_w<2, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 3: return short_chunk_w<3, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 4: return short_chunk_w<4, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    default: return short_chunk_any<V8, C16>(A, chunk, base, W, xsrc, scale_of, epi, acc);
-  }
-}
-
-// ------------------------------------------------------ long rows (bins)
-// Bin m of slice s. Thread t loads entries t + 256u of the bin (coalesced, at
-// computed addresses) and its bin-table slot; the products go to LDS; each piece is
-// then summed by one wave (lane-strided + butterfly) and handed back to thread j,
-// which owns piece j and publishes it; whoever completes a row's S slices finalises it
-// (S = 1: the piece is the row, finished in place).
-// lds: bin_cap doubles of products, kTPB ints of piece starts, kTPB piece sums.
-template <int V8, int C16, class Epi, class ScaleFn>
-__device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
-                                         const double* __restrict__ xsrc, ScaleFn scale_of,
-                                         const Epi& epi, double* lds) {
-  const int t = threadIdx.x;
-  const int bin = __builtin_amdgcn_readfirstlane(m * A.n_slices + s);  // scalar loads below
-  const int base = bin * A.bin_cap;
-  const int cbase = C16 ? A.b_cbase[bin] : 0;
-  const int hdr = A.b_hdr[bin];
-  // Issue order: the entries first (the gathers wait on them), then the bin table
-  // (its slot index waits on the header).
-  int c[kBinBatch];
-  double a[kBinBatch], xv[kBinBatch];
-#pragma unroll
-  for (int u = 0; u < kBinBatch; ++u) {
-    c[u] = col_at<C16>(A.b_col, base + u * kTPB + t, cbase);
-    a[u] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.b_val, base + u * kTPB + t);
-  }
-  __builtin_amdgcn_sched_barrier(0);
-  // only the slots up to the end marker are read (threads past it re-read the marker)
-  const int npieces = hdr & 0xFFFF, nbig = hdr >> 16;
-  const BinSeg sg = A.b_seg[bin * kTPB + (t < npieces ? t : npieces)];
-#pragma unroll
-  for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
-  // the finalising thread's own row entries travel with the gathers
-  auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
-  const Scale sc = scale_of();
-  TPL_MARK(1);
-  if (!sc.ok) return; // stopped / breakdown (uniform): slots untouched
-  // padding slots (col = -1) are never summed (pieces cover real entries only), so the
-  // product is stored unconditionally: a select here lets the compiler sink the loads
-  // of that entry into a branch and serialise them behind everything else in flight
-#pragma unroll
-  for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = a[u] * (xv[u] * sc.s);
-  keep_pre(pre);
-  for (int u0 = kBinBatch * kTPB; u0 < A.bin_cap; u0 += kBinBatch * kTPB) { // bins wider than one batch (rare)
-#pragma unroll
-    for (int u = 0; u < kBinBatch; ++u) {
-      c[u] = col_at<C16>(A.b_col, base + u0 + u * kTPB + t, cbase);
-      a[u] = val_at<V8>(A.b_val, base + u0 + u * kTPB + t);
-    }
-#pragma unroll
-    for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
-#pragma unroll
-    for (int u = 0; u < kBinBatch; ++u)
-      lds[u0 + u * kTPB + t] = a[u] * (xv[u] * sc.s);
-  }
-  int* starts = reinterpret_cast<int*>(lds + A.bin_cap);
-  double* psum = lds + A.bin_cap + kTPB / 2;  // kTPB doubles after the starts
-  starts[t] = sg.ri < 0 ? -1 - sg.start : sg.start;  // < 0: no piece (value encodes the fill)
-  __syncthreads();
-  TPL_MARK(2);
-  // Piece sums (canonical long-row order). A piece longer than kBigPiece takes a whole
-  // wave: lane l sums its entries l + 64q, then the wave butterfly. Those pieces come
-  // first in the table (nbig of them), one wave each in turn.
-  const int lane = t & 63;
-  if (!(TPL_ABLATE & 4)) {
-    for (int j = t >> 6; j < nbig; j += kTPB / 64) {
-      const int st = starts[j], nx = starts[j + 1];
-      const int en = nx >= 0 ? nx : -1 - nx;
-      double acc = 0.0;
-      for (int k0 = st + lane; k0 < en; k0 += 512) {  // 8 reads in flight, then the adds
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 64 * u < en ? k0 + 64 * u : k0];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = k0 + 64 * u < en ? acc + v[u] : acc;
-      }
-      acc = wave_sum(acc);
-      if (lane == 0) psum[j] = acc;
-    }
-  }
-  // The other pieces, 32 per pass: the 8-lane group t >> 3 takes one; its lane g sums
-  // the piece's entries g + 8q, then a butterfly over the 8 lanes.
-  const int g8 = t & 7;
-  for (int j0 = nbig; j0 < npieces; j0 += kTPB / 8) {
-    const int j = j0 + (t >> 3);
-    const int jc = j < kTPB - 2 ? j : kTPB - 2;
-    const int st = starts[jc], nx = starts[jc + 1];
-    const bool valid = j < npieces;
-    const int b0 = valid ? st : 0;
-    const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
-    double acc = 0.0;
-    if (!(TPL_ABLATE & 4)) {
-      for (int k0 = b0 + g8; k0 < en; k0 += 64) {  // 8 reads in flight, then the adds
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = k0 + 8 * u < en ? acc + v[u] : acc;
-      }
-    }
-    acc = group8_sum(acc);
-    if (g8 == 0 && valid) psum[j] = acc;
-  }
-  __syncthreads();
-  TPL_MARK(3);
-  if (sg.ri < 0) return; // no piece for this thread
-  const double p = psum[t];
-  const int ns = A.n_slices;
-  if (ns == 1) {  // the piece is the whole row: no hand-off
-    const double y = 0.0 + p;
-    if (A.long_defer) {
-      A.ypart[sg.ri] = y;
-      return;
-    }
-    double acc = 0.0;
-    epi.apply(sg.row, y, pre, acc);
-    epi.long_alpha(sg.ri, acc);
-    return;
-  }
-  // Hand-off, data-tagged: publish the piece sum write-through, drain, then read the
-  // row's S slots. The publisher whose store completed last sees all S, so
-  // some thread always finalises; a tie finalises twice, writing identical bits
-  // (every input — the slots, the row's vector entries loaded before publishing — is
-  // the same). No thread ever waits on another: nothing depends on dispatch order.
-  unsigned long long* slots = reinterpret_cast<unsigned long long*>(A.P + (size_t)sg.ri * kSlices);
-  __hip_atomic_store(slots + s, (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  TPL_MARK(4);
-  unsigned long long v[kSlices];
-#pragma unroll
-  for (int k = 0; k < kSlices; ++k)  // slots past the slice count: re-read slot 0
-    v[k] = __hip_atomic_load(slots + (k < ns ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  bool all = true;
-#pragma unroll
-  for (int k = 0; k < kSlices; ++k) all = all && v[k] != kSliceSentinel;
-  if (!all) return;
-#pragma unroll
-  for (int k = 0; k < kSlices; ++k)  // empty again for the next launch
-    if (k < ns)
-      __hip_atomic_store(slots + k, kSliceSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double y = 0.0;
-#pragma unroll
-  for (int k = 0; k < kSlices; ++k)
-    if (k < ns) y = y + __longlong_as_double((long long)v[k]);
-  if (A.long_defer) {  // partitioned: this rank's part of the row; finished after the exchange
-    A.ypart[sg.ri] = y;
-    return;
-  }
-  double acc = 0.0;
-  epi.apply(sg.row, y, pre, acc);
-  epi.long_alpha(sg.ri, acc);
-}
-
-// Minimum waves per SIMD requested for the SpMV-shaped kernels (occupancy vs VGPRs).
-#ifndef TPL_SPMV_MIN_WAVES
-#define TPL_SPMV_MIN_WAVES 1
-#endif
-#ifndef TPL_CHUNKS_FIRST
-#define TPL_CHUNKS_FIRST 0
-#endif
-// Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
-// index whose alpha partial this workgroup owns, or -1.
-// F = CW | V8 << 3 | SC16 << 4 | BC16 << 5: uniform chunk width (0: any), int8 values,
-// uint16 column offsets in the chunks / in the bins.
-template <int F, class Epi, class ScaleFn>
-__device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __restrict__ xsrc,
-                                               ScaleFn scale_of, const Epi& epi, double& acc,
-                                               double* lds) {
-  int b = blockIdx.x;
-  if (TPL_CHUNKS_FIRST) b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
-  if (b < A.n_slice_blocks) {
-    if (!(TPL_ABLATE & 1))
-      long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / A.n_slices, b % A.n_slices, xsrc, scale_of, epi, lds);
-    return -1;
-  }
-  const int chunk = b - A.n_slice_blocks;
-  if (TPL_ABLATE & 2) return -1;
-  return short_chunk<(F & 7), ((F >> 3) & 1), ((F >> 4) & 1)>(A, chunk, xsrc, scale_of, epi, acc)
-             ? chunk : -1;
-}
-
-template <int F, class Epi, class ScaleFn>
-__device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
-                                          ScaleFn scale_of, const Epi& epi, double& acc,
-                                          double* lds) {
-#if TPL_STAMP
-  TPL_MARK(0);
-  const int r = spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
-  TPL_MARK(5);
-  return r;
-#else
-  return spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
-#endif
-}
 
 // ------------------------------------------------------------------ kernels
 template <int F>
@@ -647,23 +78,28 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
                                                   double* __restrict__ Vcol, int j) {
   __shared__ double red[4];
   extern __shared__ double lds[];
-  const int stop = S.flags[0]; // checked after the loads are in flight
+  pin_layout_args(A);
+  asm volatile("" ::"s"(S.Pb_r), "s"(S.flags), "s"(S.norms), "s"(S.betas), "s"(S.Pa), "s"(A.G2_r),
+               "s"(xsrc), "s"(r_cur), "s"(r_prev), "s"(W), "s"(Vcol), "s"(j));
   PartialRegs<4> pr;           // G2 <= 1024
   load_partials(S.Pb_r, A.G2_r, pr);
-  const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
   EpiPass1 epi;
   epi.r_cur = r_cur;
   epi.r_prev = (j >= 2) ? r_prev : r_cur;
   epi.has_prev = j >= 2;
-  epi.invN_prev = (j >= 2) ? 1.0 / norm_prev : 0.0;
+  epi.invN_prev = 0.0;
   epi.invN_cur = 0.0;
   epi.beta_sub = 0.0;
   epi.W = W;
   epi.Vcol = Vcol;
   epi.Pa_long = S.Pa + A.n_chunks;
-  // beta_{j-1} (||b|| at j = 1) from the norm partials; fills the epilogue.
+  // beta_{j-1} (||b|| at j = 1) from the norm partials; fills the epilogue. Runs once the
+  // workgroup's loads are in flight: the stop flag and beta_{j-2} (DevState scalars)
+  // are waited on only here.
   auto scale_fn = [&]() -> Scale {
-    if (stop) return Scale{0.0, false};
+    __builtin_amdgcn_sched_barrier(0);
+    if (S.flags[0]) return Scale{0.0, false};
+    epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
     const double beta = sqrt(finish_partials(S.Pb_r, A.G2_r, pr, red));
     if (beta <= kBreakdownTol) {
       // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
@@ -696,12 +132,14 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   const double* __restrict__ r_cur,
                                                   double* __restrict__ r_next, int j, int k) {
   __shared__ double red[4];
-  const int stop = S.flags[0];
+  // every kernel argument in one scalar round trip
+  asm volatile("" ::"s"(A.E), "s"(A.n), "s"(A.norm_n), "s"(A.NA_r), "s"(S.Pa_r), "s"(S.flags),
+               "s"(S.norms), "s"(S.alphas), "s"(S.Pb));
+  asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k));
   PartialRegs<12> pr;
   load_partials(S.Pa_r, A.NA_r, pr);
   const int64_t beg = (int64_t)blockIdx.x * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
-  const double normj = S.norms[j - 1];
   // All of this thread's pairs (up to kAxPairs) are loaded before alpha is known, at
   // clamped addresses (vectors are padded to 64 doubles, so a pair starting below
   // `end` is always readable); the loads are unconditional so none is sunk behind the
@@ -715,6 +153,15 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     const int64_t ic = i0 < end ? i0 : beg;
     w0[q] = *reinterpret_cast<const double2*>(W + ic);
     rc0[q] = *reinterpret_cast<const double2*>(r_cur + ic);
+  }
+  // The DevState scalars (stop flag, ||r_j||) are read only now, with the vector loads
+  // in flight: waited on at entry they would add a dependent round trip.
+  __builtin_amdgcn_sched_barrier(0);
+  const int stop = S.flags[0];
+  const double normj = S.norms[j - 1];
+#pragma unroll
+  for (int q = 0; q < kAxPairs; ++q) {
+    keep(w0[q].x); keep(w0[q].y); keep(rc0[q].x); keep(rc0[q].y);
   }
   if (stop) return;
   const double alpha = finish_partials(S.Pa_r, A.NA_r, pr, red);
@@ -777,10 +224,21 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, 
                                                   double* __restrict__ Vcol, int j,
                                                   int nflush) {
   extern __shared__ double lds[];
+  pin_layout_args(A);
+  asm volatile("" ::"s"(S.betas), "s"(S.alphas), "s"(S.y), "s"(xsrc), "s"(v_cur), "s"(v_prev),
+               "s"(v_next), "s"(x), "s"(Vcol), "s"(j), "s"(nflush));
   EpiPass2 epi;
-  p2_epi_init(epi, S, v_cur, v_prev, v_next, x, Vcol, j, nflush);
+  p2_epi_ptrs(epi, v_cur, v_prev, v_next, x, Vcol, j, nflush);
+  // The coefficients are read once the workgroup's entry and vector loads are in
+  // flight (scale_of runs after them): a scalar load waited on at entry would put a
+  // second dependent round trip in front of every workgroup.
+  auto coefs = [&]() -> Scale {
+    __builtin_amdgcn_sched_barrier(0);
+    p2_epi_coefs(epi, S, j, nflush);
+    return Scale{1.0, true};
+  };
   double acc = 0.0;
-  spmv_block<F>(A, xsrc, UnitScale{}, epi, acc, lds);
+  spmv_block<F>(A, xsrc, coefs, epi, acc, lds);
 }
 
 // ---------------------------------------- replicated long rows (partitioned solve)
