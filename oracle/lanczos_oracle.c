@@ -260,12 +260,48 @@ static double nrm2_faithful(int64_t n, const double* x) {
   return s;
 }
 
+/* ------------------------------------------------------------ re-orthogonalisation */
+/* CGS2 of r against V[:, 0..cols) (column-major, ld = n), device order
+ * (k_reorth_dot / k_reorth_reduce / k_reorth_update in tpl_kernels.hip): per pass,
+ * h[c] = partials() of the G2 workgroup trees (workgroup b, thread t: acc = fma(V[c][i],
+ * r[i], acc) over i = bE + t + 256q; tree256), then r[i] = r[i] - s_i with s_i = 0;
+ * s_i = fma(V[c][i], h[c], s_i), c ascending. (Extension: the reference has no
+ * re-orthogonalisation; pinned only against this restatement and orthonormality.) */
+static void reorth_canon(const osched* S, int64_t n, const double* V, int cols, double* r,
+                         double* P, double* h) {
+  double acc[TPB];
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int c = 0; c < cols; ++c) {
+      const double* col = V + (size_t)c * (size_t)n;
+      for (int b = 0; b < S->G2; ++b) {
+        const int64_t beg = (int64_t)b * S->E;
+        const int64_t end = beg + S->E < n ? beg + S->E : n;
+        for (int t = 0; t < TPB; ++t) {
+          double a = 0.0;
+          for (int64_t i = beg + t; i < end; i += TPB) a = fma(col[i], r[i], a);
+          acc[t] = a;
+        }
+        P[b] = tree256(acc);
+      }
+      h[c] = reduce_partials(P, S->G2);
+    }
+    for (int64_t i = 0; i < n; ++i) {
+      double sum = 0.0;
+      for (int c = 0; c < cols; ++c) sum = fma(V[(size_t)c * (size_t)n + i], h[c], sum);
+      r[i] = r[i] - sum;
+    }
+  }
+}
+
 /* ------------------------------------------------------------ drivers */
 /* Standard / pass one. V (n x k, column-major) may be NULL (pass one). */
-int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, double* alphas,
-                    double* betas, size_t* steps, double* bnorm_out, double* V) {
+static int pass_one_impl(const ocsr* A, const osched* S, const double* b, size_t k,
+                         double* alphas, double* betas, size_t* steps, double* bnorm_out,
+                         double* V, int reorth) {
   const int64_t n = A->n;
   if (k == 0) return OR_BAD;
+  if (reorth && (!S || !V)) return OR_BAD;
+  double* h = reorth ? (double*)malloc(sizeof(double) * k) : NULL;
   double* P = S ? (double*)malloc(sizeof(double) * (size_t)(S->n_short + S->n_long + S->G2 + 1))
                 : NULL;
   double* vp = (double*)calloc((size_t)n + 1, sizeof(double));
@@ -275,7 +311,7 @@ int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, d
   *bnorm_out = bnorm;
   *steps = 0;
   if (bnorm <= TOL) { /* src/algorithms/mod.rs:267-273 */
-    free(P); free(vp); free(vc); free(w);
+    free(P); free(vp); free(vc); free(w); free(h);
     return OR_ZERO_B;
   }
   const double inv0 = 1.0 / bnorm;
@@ -291,6 +327,7 @@ int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, d
     *steps = it + 1;
     if (it + 1 == k) break; /* beta_k is never used */
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] - alpha * vc[i];     /* :196-198 */
+    if (reorth) reorth_canon(S, n, V, (int)(it + 1), w, P, h);        /* extension */
     const double beta = sqrt(S ? nrm2_canon(S, n, w, P) : nrm2_faithful(n, w)); /* :202 */
     if (beta <= TOL) break;                                           /* :206-208 */
     betas[nb++] = beta;
@@ -302,8 +339,18 @@ int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, d
     w = t;
     beta_prev = beta;
   }
-  free(P); free(vp); free(vc); free(w);
+  free(P); free(vp); free(vc); free(w); free(h);
   return OR_OK;
+}
+int oracle_pass_one(const ocsr* A, const osched* S, const double* b, size_t k, double* alphas,
+                    double* betas, size_t* steps, double* bnorm_out, double* V) {
+  return pass_one_impl(A, S, b, k, alphas, betas, steps, bnorm_out, V, 0);
+}
+/* lanczos_standard with CGS2 re-orthogonalisation (canonical order; V required). */
+int oracle_pass_one_reorth(const ocsr* A, const osched* S, const double* b, size_t k,
+                           double* alphas, double* betas, size_t* steps, double* bnorm_out,
+                           double* V) {
+  return pass_one_impl(A, S, b, k, alphas, betas, steps, bnorm_out, V, 1);
 }
 
 /* Pass two; y already scaled by ||b||. V (n x steps) may be NULL. */

@@ -400,6 +400,12 @@ def test_reorthogonalization_extension(op5k, kkt5k):
     R = a @ V - V @ T
     R[:, -1] = 0.0  # last column carries beta_k v_{k+1}
     assert np.linalg.norm(R) < 1e-10
+    # bitwise against the oracle's CGS2 restatement in the device order
+    al, be, st, bn, Vo = canon(op5k, a).pass_one(b, k, reorth=True)
+    assert st == s and bn == re.decomposition.b_norm
+    assert np.array_equal(re.decomposition.alphas, al)
+    assert np.array_equal(re.decomposition.betas, be)
+    assert np.array_equal(np.asarray(V), Vo)
 
 
 def test_device_pointer_path(op5k, kkt5k):

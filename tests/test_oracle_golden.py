@@ -198,3 +198,24 @@ def test_canonical_and_faithful_agree_before_chaos(kkt5k):
     xc = oracle.Operator(a, canon_schedule(a)).lanczos_two_pass(b, 50, ftk_ref.inv)
     xf = oracle.Operator(a).lanczos_two_pass(b, 50, ftk_ref.inv)
     assert np.linalg.norm(xc - xf) / np.linalg.norm(xf) < 1e-10
+
+
+def test_oracle_reorth_restatement(kkt5k):
+    """The CGS2 restatement (extension, BASELINE configs[3]) keeps V_k orthonormal where
+    the plain recurrence has lost orthogonality, agrees with it before the loss, and
+    satisfies the Lanczos relation A V = V T + beta_k v_{k+1} e_k^T."""
+    a = kkt5k.a
+    b = std_rng_vector(a.shape[0])
+    o = oracle.Operator(a, canon_schedule(a))
+    k = 120
+    al, be, st, bn, V = o.pass_one(b, k, reorth=True)
+    alp, bep, stp, bnp, Vp = o.pass_one(b, k, store_basis=True)
+    assert st == stp == k and bn == bnp
+    assert np.linalg.norm(np.eye(st) - V.T @ V) < 1e-13
+    assert np.linalg.norm(np.eye(stp) - Vp.T @ Vp) > 1e-6
+    assert np.allclose(al[:8], alp[:8], atol=1e-12) and np.allclose(be[:8], bep[:8], rtol=1e-12)
+    R = a @ V - V @ ftk_ref.tridiag(al, be)
+    R[:, -1] = 0.0
+    assert np.linalg.norm(R) < 1e-10
+    with pytest.raises(ValueError):
+        oracle.Operator(a).pass_one(b, 5, reorth=True)  # canonical order only

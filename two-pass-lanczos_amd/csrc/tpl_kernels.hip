@@ -324,15 +324,18 @@ __global__ __launch_bounds__(kTPB) void k_gemv_recon(int64_t n, int steps, DevSt
 // Gram-Schmidt applied twice (CGS2) of r_{j+1} against V_k[:, 0..cols) before
 // beta_j is formed. V is column-major (ld = n): lane i of a wave reads V[c*n + i],
 // so every column sweep is a coalesced stream.
-constexpr int kReorthCols = 8; // columns per workgroup in the h = V^T r kernel
+constexpr int kReorthCols = 16; // columns per workgroup in the h = V^T r kernel
 
-// h partials: grid (G2, ceil(cols/8)); workgroup (b, g) owns rows [bE, min(n,(b+1)E))
-// and columns [8g, 8g+8). P[c*G2 + b] = tree256 of the thread accumulators.
+// h partials: grid (G2, ceil(cols/16)); workgroup (b, g) owns rows [bE, min(n,(b+1)E))
+// and columns [16g, 16g+16). P[c*G2 + b] = tree256 of the thread accumulators (thread
+// t: acc = fma(V[c][i], r[i], acc) over i = bE + t + 256q, q ascending). Every column's
+// load is issued unconditionally (columns past cols re-read column 16g, unused) so the
+// 17 loads of an iteration are all in flight; the 16 trees share one barrier.
 __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
                                                      const double* __restrict__ V,
                                                      const double* __restrict__ r,
                                                      double* __restrict__ P, int G, int64_t E) {
-  __shared__ double red[4];
+  __shared__ double red[kReorthCols * 4];
   const int c0 = blockIdx.y * kReorthCols;
   const int nc = cols - c0 < kReorthCols ? cols - c0 : kReorthCols;
   const int64_t beg = (int64_t)blockIdx.x * E;
@@ -340,17 +343,26 @@ __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
   double acc[kReorthCols];
 #pragma unroll
   for (int u = 0; u < kReorthCols; ++u) acc[u] = 0.0;
+#pragma unroll 2
   for (int64_t i = beg + threadIdx.x; i < end; i += kTPB) {
     const double ri = r[i];
+    double v[kReorthCols];
 #pragma unroll
-    for (int u = 0; u < kReorthCols; ++u)
-      if (u < nc) acc[u] = fma(V[(int64_t)(c0 + u) * n + i], ri, acc[u]);
+    for (int u = 0; u < kReorthCols; ++u) v[u] = V[(int64_t)(c0 + (u < nc ? u : 0)) * n + i];
+#pragma unroll
+    for (int u = 0; u < kReorthCols; ++u) acc[u] = u < nc ? fma(v[u], ri, acc[u]) : acc[u];
   }
+  const int w = threadIdx.x >> 6;
 #pragma unroll
   for (int u = 0; u < kReorthCols; ++u) {
-    const double s = block_sum(acc[u], red);
-    if (u < nc && threadIdx.x == 0) P[(int64_t)(c0 + u) * G + blockIdx.x] = s;
+    const double sw = wave_sum(acc[u]);
+    if ((threadIdx.x & 63) == 0) red[u * 4 + w] = sw;
   }
+  __syncthreads();
+  const int u = threadIdx.x;
+  if (u < nc)
+    P[(int64_t)(c0 + u) * G + blockIdx.x] =
+        (red[u * 4 + 0] + red[u * 4 + 1]) + (red[u * 4 + 2] + red[u * 4 + 3]);
 }
 
 // h[c] = sum of the G partials of column c (one workgroup per column).
@@ -365,6 +377,12 @@ __global__ __launch_bounds__(kTPB) void k_reorth_reduce(const double* __restrict
 }
 
 // r -= V h ; optional ||r||^2 partials in the canonical norm order (E partition).
+// Thread t owns the pairs (i0, i0 + 1), i0 = bE + 2t + 512q, as the norm order does;
+// per element s = 0; s = fma(V[c][i], h[c], s) for c ascending. The columns are taken
+// kUpdCols at a time with all 2 kUpdCols loads in flight before the ordered FMAs: the
+// sweep is a pure HBM stream (V_j does not fit the Infinity Cache at k = 500), so bytes
+// in flight per CU, not arithmetic, set its rate.
+constexpr int kUpdCols = 16;
 __global__ __launch_bounds__(kTPB) void k_reorth_update(int64_t n, int cols,
                                                         const double* __restrict__ V,
                                                         double* __restrict__ r,
@@ -375,15 +393,37 @@ __global__ __launch_bounds__(kTPB) void k_reorth_update(int64_t n, int cols,
   const int64_t end = beg + E < n ? beg + E : n;
   double acc = 0.0;
   for (int64_t i0 = beg + 2 * threadIdx.x; i0 < end; i0 += 2 * kTPB) {
-    for (int e = 0; e < 2; ++e) {
-      const int64_t i = i0 + e;
-      if (i < end) {
-        double s = 0.0;
-        for (int c = 0; c < cols; ++c) s = fma(V[(int64_t)c * n + i], h[c], s);
-        const double ri = r[i] - s;
-        r[i] = ri;
-        acc = fma(ri, ri, acc);
+    const bool has1 = i0 + 1 < end;
+    const int64_t i1 = has1 ? i0 + 1 : i0;
+    const double r0 = r[i0], r1 = r[i1];
+    double s0 = 0.0, s1 = 0.0;
+    int c = 0;
+    for (; c + kUpdCols <= cols; c += kUpdCols) {
+      double v0[kUpdCols], v1[kUpdCols];
+#pragma unroll
+      for (int u = 0; u < kUpdCols; ++u) {
+        const double* col = V + (int64_t)(c + u) * n;
+        v0[u] = col[i0];
+        v1[u] = col[i1];
       }
+#pragma unroll
+      for (int u = 0; u < kUpdCols; ++u) {
+        s0 = fma(v0[u], h[c + u], s0);
+        s1 = fma(v1[u], h[c + u], s1);
+      }
+    }
+    for (; c < cols; ++c) {
+      const double* col = V + (int64_t)c * n;
+      s0 = fma(col[i0], h[c], s0);
+      s1 = fma(col[i1], h[c], s1);
+    }
+    const double q0 = r0 - s0;
+    r[i0] = q0;
+    acc = fma(q0, q0, acc);
+    if (has1) {
+      const double q1 = r1 - s1;
+      r[i1] = q1;
+      acc = fma(q1, q1, acc);
     }
   }
   if (Pnorm) {
