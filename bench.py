@@ -9,13 +9,16 @@ pass two), the window the reference times (src/bin/tradeoff.rs:265-288). Inputs
 
     python bench.py [--gpus N --steps K --warmup W]
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): every rank runs its own
-full-size replica of the workload (no data-path collective),
-timed between barriers, max over ranks; value = all ranks' iterations / that time.
+N > 1 (launched by torch.distributed.run, one rank per GPU): the ranks run ONE
+row-partitioned solve of BASELINE configs[4] (5M-arc synthetic KKT, k = 500) together
+(strong scaling), timed between barriers, max over ranks; rank 0 then
+times the same workload on its GPU alone (single_gpu_same_workload).
 
 Extra JSON fields: ``roofline`` for the dominant kernel (algorithmic bytes per launch /
 HIP-event average launch time, vs 8 TB/s HBM3E), ``cpu_baseline`` (the oracle's
-reference-order restatement, single core, bounded sample on the host of the GPU box).
+reference-order restatement, single core, bounded sample on the host of the GPU box),
+``one_pass_reorth`` (BASELINE configs[3]: one-pass k = 500 with CGS2 re-orthogonalisation,
+its sweep rate against HBM).
 """
 from __future__ import annotations
 
@@ -49,6 +52,9 @@ def parse():
     p.add_argument("--cpu-k", type=int, default=500, help="k of the bounded CPU sample")
     p.add_argument("--cpu-reps", type=int, default=2, help="CPU sample repetitions")
     p.add_argument("--profile-iters", type=int, default=200)
+    p.add_argument("--one-pass", type=int, default=1,
+                   help="N=1: also time BASELINE configs[3] (one-pass k with CGS2 "
+                        "re-orthogonalisation, V_k in HBM); 0 to skip")
     return p.parse_args()
 
 
@@ -221,6 +227,40 @@ def main():
 
     if single is not None:
         out["single_gpu_same_workload"] = single
+    if args.one_pass and not partitioned:
+        # BASELINE configs[3]: lanczos_standard (one pass, V_k in HBM) with CGS2 full
+        # re-orthogonalisation, same instance and k; V stays on the device. The sweep
+        # rate counts the algorithmic bytes of the re-orthogonalisation (per step j, two
+        # passes of h = V_j^T r and r -= V_j h: 2 (16 n j + 24 n) bytes) over the time the
+        # solve spends beyond the plain one-pass solve.
+        import ctypes
+        PD = ctypes.POINTER(ctypes.c_double)
+        al, be = np.zeros(args.k), np.zeros(args.k)
+        st, bn = ctypes.c_size_t(0), ctypes.c_double(0.0)
+
+        def one_pass(reorth):
+            check(_lib.tpl_lanczos_standard(op.handle, b_dev.data_ptr(), nloc, args.k,
+                                            al.ctypes.data_as(PD), be.ctypes.data_as(PD),
+                                            ctypes.byref(st), ctypes.byref(bn), None,
+                                            _lib.TPL_MEM_DEVICE, reorth, None, None))
+            torch.cuda.synchronize()
+
+        tm = {}
+        for reorth in (0, 1):
+            one_pass(reorth)
+            t1 = time.perf_counter()
+            for _ in range(2):
+                one_pass(reorth)
+            tm[reorth] = (time.perf_counter() - t1) / 2
+        s1 = int(st.value)
+        rb = sum(2.0 * (16.0 * n * j + 24.0 * n) for j in range(1, s1))
+        rate = rb / max(tm[1] - tm[0], 1e-9) / 1e9
+        out["one_pass_reorth"] = {
+            "config": f"lanczos_standard k={args.k} + CGS2, V_k in HBM ({8 * n * args.k / 1e9:.2f} GB)",
+            "ms_per_solve": round(1000 * tm[1], 2), "iterations_per_s": round(s1 / tm[1], 1),
+            "plain_one_pass_ms": round(1000 * tm[0], 3),
+            "reorth_bytes": rb, "reorth_GBs": round(rate, 1),
+            "reorth_frac_of_hbm": round(rate / HBM_PEAK_GBS, 4)}
     if rank == 0 and args.cpu_baseline and world == 1 and not partitioned:
         import oracle  # CPU baseline only (reference-order restatement, single thread)
         from oracle import ftk_ref

@@ -14,11 +14,12 @@ a = load_kkt_system(os.path.join(ROOT, "tests/golden/kkt/netgen-500000-3.dmx.xz"
 n = a.shape[0]
 b = a @ np.full(n, 1 / np.sqrt(n))
 op = tpl_amd.HipCsrOp(a)
+op.set_push(True)
 tpl_amd.lanczos_two_pass(op, b, 50, "inv")
 sch = op.schedule()
 assert sch["push"], sch["push"]
 nch = -(-len(sch["short_rows"]) // sch["chunk_rows"])
-ncomb = -(-len(sch["long_rows"]) // 16)
+ncomb = -(-len(sch["long_rows"]) // 32)  # kCombRows
 fn = _lib.lib.tpl_debug_stamps_push
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 def q(x):

@@ -21,8 +21,16 @@ n = a.shape[0]
 b = a @ np.full(n, 1 / np.sqrt(n))
 op = tpl_amd.HipCsrOp(a)
 op.set_slices(int(os.environ.get("SLICES", "0")))
+op.set_push(os.environ.get("PUSH", "0") == "1")
 tpl_amd.lanczos_two_pass(op, b, 50, "inv")
-row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "slices": op.schedule()["slices"]}
+row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "slices": op.schedule()["slices"], "push": op.pushed}
+if os.environ.get("SOLVE", "1") == "1":  # full two-pass k=500 solves (ms, best of 5)
+    import time
+    tpl_amd.lanczos_two_pass(op, b, 500, "inv")
+    ts = []
+    for _ in range(5):
+        t0 = time.perf_counter(); tpl_amd.lanczos_two_pass(op, b, 500, "inv"); ts.append(time.perf_counter() - t0)
+    row["solve_ms"] = round(1000 * min(ts), 3)
 for kid, nm in [(0, "p1_spmv"), (1, "p1_axpy"), (2, "p2_spmv"), (3, "spmv")]:
     us, by = op.profile_kernel(kid, 300)
     row[nm] = round(us, 2)

@@ -121,6 +121,26 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
   return block_sum(s, red);
 }
 
+// Vector results of a step (w, v_{j+1}, x, r_{j+1}) are consumed only by the NEXT
+// launch. Stored write-through (agent-scope relaxed stores: global_store ... sc1) they
+// leave the XCD's L2 while the kernel runs, instead of as dirty lines written back at
+// the kernel boundary (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s).
+#ifndef TPL_WT_STORES
+#define TPL_WT_STORES 1
+#endif
+#ifndef TPL_WT_AXPY
+#define TPL_WT_AXPY 0  // r_{j+1} of k_p1_axpy: 16-B plain stores (measured faster)
+#endif
+__device__ __forceinline__ void st_out(double* p, double v) {
+#if TPL_WT_STORES
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
+                     (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+#else
+  *p = v;
+#endif
+}
+
 // Pins a value as computed unconditionally: without it the compiler sinks the loads
 // feeding a product used under a select (padding entries) into a branch, where they
 // issue late behind an s_waitcnt vmcnt(0) and serialise the workgroup's round trips.
@@ -134,7 +154,7 @@ struct EpiSpmv {
   double* y;
   __device__ __forceinline__ PreNone pre(int) const { return {}; }
   __device__ __forceinline__ double apply(int i, double s, const PreNone&, double&) const {
-    y[i] = s;
+    st_out(y + i, s);
     return s;
   }
   __device__ __forceinline__ void long_alpha(int, double) const {}
@@ -160,7 +180,7 @@ struct EpiPass1 {
     const double v = p.rc * invN_cur;
     const double vp = has_prev ? p.rp * invN_prev : 0.0;
     const double w = s - beta_sub * vp;
-    W[i] = w;
+    st_out(W + i, w);
     if (Vcol) Vcol[i] = v;
     acc = fma(v, w, acc);
     return v;
@@ -194,12 +214,12 @@ struct EpiPass2 {
     double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
-    v_next[i] = vn;
+    st_out(v_next + i, vn);
     if (nflush) {
       double xv = p.x;
       if (nflush >= 3) xv = xv + ycoef2 * p.vp;
       if (nflush >= 2) xv = xv + ycoef1 * p.vc;
-      x[i] = xv + ycoef * vn;
+      st_out(x + i, xv + ycoef * vn);
     }
     if (Vcol) Vcol[i] = vn;
     return vn;

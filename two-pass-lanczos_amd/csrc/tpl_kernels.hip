@@ -176,11 +176,16 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     double2 r;
     r.x = w.x - alpha * (rc.x * invN);
     r.y = w.y - alpha * (rc.y * invN);
+#if TPL_WT_AXPY
+    st_out(r_next + i0, r.x);
+    if (i0 + 1 < end) st_out(r_next + i0 + 1, r.y);
+#else
     if (i0 + 1 < end) {
       *reinterpret_cast<double2*>(r_next + i0) = r;
     } else {
       r_next[i0] = r.x;
     }
+#endif
     acc = i0 < A.norm_n ? fma(r.x, r.x, acc) : acc;
     acc = i0 + 1 < end && i0 + 1 < A.norm_n ? fma(r.y, r.y, acc) : acc;
   };
