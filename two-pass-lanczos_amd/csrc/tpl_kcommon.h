@@ -582,6 +582,21 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   epi.long_alpha(sg.ri, acc);
 }
 
+// XCD-affine chunk order (speed only; any bijection is correct). Workgroups are dealt
+// round-robin to the 8 XCDs, block B on XCD B % 8 (observed on every launch: block 0
+// on XCD 0, scripts/lab/xcd_rr.hip), and an XCD's L2 keeps the lines a kernel wrote
+// there for the next kernel (scripts/lab/l2_keep.hip: 32 MB re-read 7.4 us on the
+// writing XCD vs 10.4 us elsewhere). Short chunk c (512 rows) lies in element-wise block
+// c / 2 (E = 1024 rows), which k_p1_axpy / k_p1_init run on XCD (c / 2) % 8; the chunk
+// part of an SpMV grid (padded to a multiple of 16) places chunk c = 16q + 2x + e on a
+// block of XCD x, so the rows' vectors (r, w, v, x) stay in one XCD's L2 from launch
+// to launch. i: block index within the chunk part; returns -1 for padding blocks.
+__device__ __forceinline__ int chunk_of_block(const CsrDev& A, int i) {
+  const int x = ((i & 7) + A.n_slice_blocks) & 7;
+  const int c = (i >> 4) * 16 + 2 * x + ((i >> 3) & 1);
+  return c < A.n_chunks ? c : -1;
+}
+
 // Minimum waves per SIMD requested for the SpMV-shaped kernels (occupancy vs VGPRs).
 #ifndef TPL_SPMV_MIN_WAVES
 #define TPL_SPMV_MIN_WAVES 1
@@ -604,8 +619,8 @@ __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __
       long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / A.n_slices, b % A.n_slices, xsrc, scale_of, epi, lds);
     return -1;
   }
-  const int chunk = b - A.n_slice_blocks;
-  if (TPL_ABLATE & 2) return -1;
+  const int chunk = chunk_of_block(A, b - A.n_slice_blocks);
+  if (chunk < 0 || (TPL_ABLATE & 2)) return -1;  // grid padding
   return short_chunk<(F & 7), ((F >> 3) & 1), ((F >> 4) & 1)>(A, chunk, xsrc, scale_of, epi, acc)
              ? chunk : -1;
 }

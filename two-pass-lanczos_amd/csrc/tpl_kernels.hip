@@ -449,7 +449,8 @@ static inline int elem_grid(int64_t n) {
   if (g < 1) g = 1;
   return (int)g;
 }
-static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + A.n_chunks; }
+// chunk part padded to a multiple of 16 (chunk_of_block in tpl_kcommon.h)
+static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + (A.n_chunks + 15) / 16 * 16; }
 // dynamic LDS of the SpMV-shaped kernels: a bin's staged products + piece starts
 static inline size_t spmv_lds_bytes(const CsrDev& A) {
   return A.n_slice_blocks > 0
