@@ -209,7 +209,7 @@ tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_short, int32_t* n_long, int32
 tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g2);
 /* Column slices S of the long rows (1, 2, 4 or 8; part of the canonical reduction
  * order). tpl_op_set_slices rebuilds the layout with an explicit S
- * (0 = the auto rule: the fewest slices whose share of the vector fits half an L2,
+ * (0 = the auto rule: the fewest slices whose share of the vector fits a quarter of an L2,
  * more if a (row, slice) piece would not fit one bin).                          */
 tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices);
 tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices);

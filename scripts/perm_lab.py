@@ -34,16 +34,20 @@ orders = {
     "head": np.lexsort((tail, head)),
     "min": np.lexsort((np.maximum(c0, c1), np.minimum(c0, c1))),
 }
-for name, o in orders.items():
+for name, o in [(k, orders[k]) for k in os.environ.get("ORDERS", "orig,min,tail").split(",")]:
     perm = np.concatenate([arc_rows[o], node_rows])
     ap = sp.csr_matrix(a[perm][:, perm])
     ap.sort_indices()
     b = ap @ np.full(n, 1 / np.sqrt(n))
-    for s in (1, 2, 4, 8):
+    for s in [int(v) for v in os.environ.get("SLICES", "2,4").split(",")]:
         op = tpl_amd.HipCsrOp(ap)
         op.set_slices(s)
-        tpl_amd.lanczos_two_pass(op, b, 50, "inv")
-        row = {"order": name, "slices": s}
+        tpl_amd.lanczos_two_pass(op, b, 500, "inv")
+        import time
+        ts = []
+        for _ in range(4):
+            t0 = time.perf_counter(); tpl_amd.lanczos_two_pass(op, b, 500, "inv"); ts.append(time.perf_counter() - t0)
+        row = {"order": name, "slices": s, "solve_ms": round(1000 * min(ts), 3)}
         for kid, nm in [(0, "p1_spmv"), (1, "p1_axpy"), (2, "p2_spmv")]:
             us, _ = op.profile_kernel(kid, 300)
             row[nm] = round(us, 2)

@@ -158,11 +158,11 @@ def push_rows_per_thread(a, short, long_, max_long=2048):
 
 def auto_slices(a, long_rows, bin_max=7936):
     """tpl_runtime.cpp auto_slices + build_layout: the fewest of 1, 2, 4, 8 column slices
-    whose share of the vector (8 n bytes) fits 2 MiB, doubled while a (long row, slice)
+    whose share of the vector (8 n bytes) fits 1 MiB, doubled while a (long row, slice)
     piece holds more than bin_max entries."""
     n = a.shape[0]
     s = 1
-    while s < 8 and n * 8.0 / s > 2.0 * 1024 * 1024:
+    while s < 8 and n * 8.0 / s > 1.0 * 1024 * 1024:
         s *= 2
 
     def widest(S):

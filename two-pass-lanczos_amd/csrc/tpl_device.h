@@ -13,7 +13,7 @@
 //     computed, not loaded, and the kernel is specialised for W.
 //   * LONG rows are cut into S column slices [floor(n*s/S), floor(n*(s+1)/S)), S in
 //     {1, 2, 4, 8} (tpl_runtime.cpp auto_slices: the fewest whose share of the
-//     gathered vector fits half an L2). The (row, slice) pieces of slice s, long
+//     gathered vector fits a quarter of an L2). The (row, slice) pieces of slice s, long
 //     rows ascending, are packed whole into BINS of bin_cap entries (padding
 //     col = -1) with at most kBinSegs pieces each; every slice gets the same number
 //     M of bins. Bin m of slice s is workgroup S*m + s of the slice part of the
@@ -80,6 +80,8 @@ constexpr int kBigPiece = 64;
 constexpr int kBinMin = TPL_BIN_MIN; // default entries per bin
 constexpr int kBinBatch = kBinMin / kTPB;  // entries per thread per load batch
 constexpr int kLongEpiRows = 1024;
+constexpr int kWinMax = 2048;        // short-chunk column window in LDS: at most this many columns
+constexpr int kWinLoads = kWinMax / 256;  // window loads per thread
 constexpr int kPushTPB = 512;        // threads per pushed-chunk / combiner workgroup (8 waves)
 constexpr int kCombRows = kPushTPB / 16;  // long rows per combiner workgroup (16 lanes each)
 constexpr int kPushMaxLong = 2048;   // pushed long rows: at most this many long rows
@@ -160,6 +162,11 @@ struct CsrDev {
   int32_t push_rpt;         // short rows per thread (chunk = kPushTPB * push_rpt positions)
   int32_t n_comb;           // combiner workgroups = ceil(n_long / kCombRows)
   int32_t tp_cap;           // LDS product slots (max pushed entries of one chunk)
+  // Short-chunk column window (s_win > 0: every chunk's columns lie in [cbase, cbase +
+  // s_win), s_win <= kWinMax; the window is staged in LDS). s_win_max: the largest
+  // column of any chunk (window loads past it are clamped there).
+  int32_t s_win;
+  int32_t s_win_max;
 };
 
 // Device-resident solver state (one per operator).

@@ -131,6 +131,13 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
 #ifndef TPL_WT_AXPY
 #define TPL_WT_AXPY 0  // r_{j+1} of k_p1_axpy: 16-B plain stores (measured faster)
 #endif
+#ifndef TPL_WT_W
+#define TPL_WT_W 1  // pass one's w (read next by k_p1_axpy on the same XCD only)
+#endif
+#ifndef TPL_WT_X
+#define TPL_WT_X 1  // pass two's x (read again three steps later, same XCD only)
+#endif
+__device__ __forceinline__ void st_plain(double* p, double v) { *p = v; }
 __device__ __forceinline__ void st_out(double* p, double v) {
 #if TPL_WT_STORES
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
@@ -180,7 +187,11 @@ struct EpiPass1 {
     const double v = p.rc * invN_cur;
     const double vp = has_prev ? p.rp * invN_prev : 0.0;
     const double w = s - beta_sub * vp;
+#if TPL_WT_W
     st_out(W + i, w);
+#else
+    st_plain(W + i, w);
+#endif
     if (Vcol) Vcol[i] = v;
     acc = fma(v, w, acc);
     return v;
@@ -219,7 +230,11 @@ struct EpiPass2 {
       double xv = p.x;
       if (nflush >= 3) xv = xv + ycoef2 * p.vp;
       if (nflush >= 2) xv = xv + ycoef1 * p.vc;
+#if TPL_WT_X
       st_out(x + i, xv + ycoef * vn);
+#else
+      st_plain(x + i, xv + ycoef * vn);
+#endif
     }
     if (Vcol) Vcol[i] = vn;
     return vn;
@@ -300,12 +315,24 @@ __device__ __forceinline__ int col_at(const void* p, int i, int base) {
 // ------------------------------------------------------ short rows (sliced ELL)
 // Chunk with a compile-time width W (entries loaded unconditionally: the sliced-ELL
 // storage is allocated for whole chunks, padding has col = -1).
-template <int W, int V8, int C16, class Epi, class ScaleFn>
+template <int W, int V8, int C16, int WIN, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int base,
                                               const double* __restrict__ xsrc, ScaleFn scale_of,
-                                              const Epi& epi, double& acc) {
+                                              const Epi& epi, double& acc, double* lds) {
   const int t = threadIdx.x;
   const int cbase = C16 ? A.s_cbase[chunk] : 0;
+  // WIN: the chunk's column window [cbase, cbase + s_win) is loaded coalesced into LDS
+  // (issued first, in parallel with the entries) and gathered from there: the KKT arc
+  // rows' columns all lie in the 1,155 node columns, so ~1 M divergent L1 gathers per
+  // SpMV become LDS reads and the chunk's chain shrinks to one memory round trip.
+  double wv[WIN ? kWinLoads : 1];
+  if (WIN) {
+#pragma unroll
+    for (int u = 0; u < kWinLoads; ++u) {
+      const int k = t + u * kTPB;
+      wv[u] = xsrc[cbase + k < A.s_win_max ? cbase + k : A.s_win_max];
+    }
+  }
   int row[kRowsPerThread];
   bool live[kRowsPerThread];
   decltype(epi.pre(0)) pre[kRowsPerThread];
@@ -332,10 +359,21 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
 #endif
+  if (WIN) {
 #pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q)
+    for (int u = 0; u < kWinLoads; ++u)
+      if (t + u * kTPB < A.s_win) lds[t + u * kTPB] = wv[u];
+    __syncthreads();
 #pragma unroll
-    for (int k = 0; k < W; ++k) xv[q][k] = xsrc[(TPL_ABLATE & 16) ? (cbase + (t & 63)) : (c[q][k] < 0 ? 0 : c[q][k])];
+    for (int q = 0; q < kRowsPerThread; ++q)
+#pragma unroll
+      for (int k = 0; k < W; ++k) xv[q][k] = lds[c[q][k] < 0 ? 0 : c[q][k] - cbase];
+  } else {
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q)
+#pragma unroll
+      for (int k = 0; k < W; ++k) xv[q][k] = xsrc[(TPL_ABLATE & 16) ? (cbase + (t & 63)) : (c[q][k] < 0 ? 0 : c[q][k])];
+  }
 #if TPL_PRE_LATE
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
@@ -406,12 +444,13 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
 
 // CW > 0: the kernel was specialised for a uniform chunk width CW (tpl::launch picks
 // it from A.s_width); CW == 0: generic, any per-chunk width.
-template <int CW, int V8, int C16, class Epi, class ScaleFn>
+template <int CW, int V8, int C16, int WIN, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
                                             const double* __restrict__ xsrc, ScaleFn scale_of,
-                                            const Epi& epi, double& acc) {
+                                            const Epi& epi, double& acc, double* lds) {
   if (CW > 0)
-    return short_chunk_w<CW, V8, C16>(A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc);
+    return short_chunk_w<CW, V8, C16, (CW > 0 && C16) ? WIN : 0>(
+        A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc, lds);
   int W, base;
   if (A.s_width > 0) {
     W = A.s_width;
@@ -421,10 +460,10 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
     base = A.c_base[chunk];
   }
   switch (W) {
-    case 1: return short_chunk_w<1, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 2: return short_chunk_w<2, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 3: return short_chunk_w<3, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
-    case 4: return short_chunk_w<4, V8, C16>(A, chunk, base, xsrc, scale_of, epi, acc);
+    case 1: return short_chunk_w<1, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 2: return short_chunk_w<2, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 3: return short_chunk_w<3, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 4: return short_chunk_w<4, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
     default: return short_chunk_any<V8, C16>(A, chunk, base, W, xsrc, scale_of, epi, acc);
   }
 }
@@ -606,8 +645,8 @@ __device__ __forceinline__ int chunk_of_block(const CsrDev& A, int i) {
 #endif
 // Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
 // index whose alpha partial this workgroup owns, or -1.
-// F = CW | V8 << 3 | SC16 << 4 | BC16 << 5: uniform chunk width (0: any), int8 values,
-// uint16 column offsets in the chunks / in the bins.
+// F = CW | V8 << 3 | SC16 << 4 | BC16 << 5 | WIN << 6: uniform chunk width (0: any), int8
+// values, uint16 column offsets in the chunks / in the bins, chunk column window in LDS.
 template <int F, class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __restrict__ xsrc,
                                                ScaleFn scale_of, const Epi& epi, double& acc,
@@ -621,7 +660,7 @@ __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __
   }
   const int chunk = chunk_of_block(A, b - A.n_slice_blocks);
   if (chunk < 0 || (TPL_ABLATE & 2)) return -1;  // grid padding
-  return short_chunk<(F & 7), ((F >> 3) & 1), ((F >> 4) & 1)>(A, chunk, xsrc, scale_of, epi, acc)
+  return short_chunk<(F & 7), ((F >> 3) & 1), ((F >> 4) & 1), ((F >> 6) & 1)>(A, chunk, xsrc, scale_of, epi, acc, lds)
              ? chunk : -1;
 }
 

@@ -453,9 +453,11 @@ static inline int elem_grid(int64_t n) {
 static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + (A.n_chunks + 15) / 16 * 16; }
 // dynamic LDS of the SpMV-shaped kernels: a bin's staged products + piece starts
 static inline size_t spmv_lds_bytes(const CsrDev& A) {
-  return A.n_slice_blocks > 0
+  const size_t bins = A.n_slice_blocks > 0
              ? (size_t)A.bin_cap * sizeof(double) + kTPB * sizeof(int) + kTPB * sizeof(double)
              : 0;
+  const size_t win = (size_t)A.s_win * sizeof(double);  // short-chunk column window
+  return bins > win ? bins : win;
 }
 // Launch the SpMV-shaped kernel specialised for the layout's uniform chunk width.
 #define TPL_LAUNCH_CASE(KERNEL, F)                                                          \
@@ -467,7 +469,8 @@ static inline size_t spmv_lds_bytes(const CsrDev& A) {
     const size_t shm_ = spmv_lds_bytes(A);                                                  \
     hipStream_t s_ = (s);                                                                   \
     const int cw_ = (A).s_width >= 1 && (A).s_width <= 4 ? (A).s_width : 0;                \
-    switch (cw_ | ((A).val_i8 ? 8 : 0) | ((A).s_col16 ? 16 : 0) | ((A).b_col16 ? 32 : 0)) { \
+    switch (cw_ | ((A).val_i8 ? 8 : 0) | ((A).s_col16 ? 16 : 0) | ((A).b_col16 ? 32 : 0) |  \
+            ((A).s_win > 0 && cw_ > 0 && (A).s_col16 ? 64 : 0)) {                            \
       TPL_LAUNCH_CASE(KERNEL, 0); TPL_LAUNCH_CASE(KERNEL, 32); TPL_LAUNCH_CASE(KERNEL, 16); TPL_LAUNCH_CASE(KERNEL, 48);\
       TPL_LAUNCH_CASE(KERNEL, 8); TPL_LAUNCH_CASE(KERNEL, 40); TPL_LAUNCH_CASE(KERNEL, 24); TPL_LAUNCH_CASE(KERNEL, 56);\
       TPL_LAUNCH_CASE(KERNEL, 1); TPL_LAUNCH_CASE(KERNEL, 33); TPL_LAUNCH_CASE(KERNEL, 17); TPL_LAUNCH_CASE(KERNEL, 49);\
@@ -478,6 +481,10 @@ static inline size_t spmv_lds_bytes(const CsrDev& A) {
       TPL_LAUNCH_CASE(KERNEL, 11); TPL_LAUNCH_CASE(KERNEL, 43); TPL_LAUNCH_CASE(KERNEL, 27); TPL_LAUNCH_CASE(KERNEL, 59);\
       TPL_LAUNCH_CASE(KERNEL, 4); TPL_LAUNCH_CASE(KERNEL, 36); TPL_LAUNCH_CASE(KERNEL, 20); TPL_LAUNCH_CASE(KERNEL, 52);\
       TPL_LAUNCH_CASE(KERNEL, 12); TPL_LAUNCH_CASE(KERNEL, 44); TPL_LAUNCH_CASE(KERNEL, 28); TPL_LAUNCH_CASE(KERNEL, 60);\
+      TPL_LAUNCH_CASE(KERNEL, 81); TPL_LAUNCH_CASE(KERNEL, 82); TPL_LAUNCH_CASE(KERNEL, 83); TPL_LAUNCH_CASE(KERNEL, 84);\
+      TPL_LAUNCH_CASE(KERNEL, 89); TPL_LAUNCH_CASE(KERNEL, 90); TPL_LAUNCH_CASE(KERNEL, 91); TPL_LAUNCH_CASE(KERNEL, 92);\
+      TPL_LAUNCH_CASE(KERNEL, 113); TPL_LAUNCH_CASE(KERNEL, 114); TPL_LAUNCH_CASE(KERNEL, 115); TPL_LAUNCH_CASE(KERNEL, 116);\
+      TPL_LAUNCH_CASE(KERNEL, 121); TPL_LAUNCH_CASE(KERNEL, 122); TPL_LAUNCH_CASE(KERNEL, 123); TPL_LAUNCH_CASE(KERNEL, 124);\
       default: break;                                                                   \
     }                                                                                       \
   }(__VA_ARGS__)

@@ -120,12 +120,14 @@ struct SchedParams {
 };
 
 // Column slices of the long rows (auto rule): the fewest (1, 2, 4, 8) whose share of
-// the gathered vector fits in half an XCD's 4 MiB L2 — slice s runs on the XCDs
+// the gathered vector fits in a quarter of an XCD's 4 MiB L2 (measured at 500k arcs:
+// 4 slices 12.9 ms per k = 500 solve, 2 slices 13.5, 8 slices 15.4; at 50k: 1 slice
+// 7.1 ms, 2 slices 9.1) — slice s runs on the XCDs
 // b % 8 == s (mod slices), so each L2 caches only its slice's columns — and, when a
 // (row, slice) piece would exceed one bin, more slices until every piece fits.
 static int auto_slices(int64_t n_cols) {
   int s = 1;
-  while (s < kSlices && (double)n_cols * 8.0 / s > 2.0 * 1024.0 * 1024.0) s *= 2;
+  while (s < kSlices && (double)n_cols * 8.0 / s > 1.0 * 1024.0 * 1024.0) s *= 2;
   return s;
 }
 
@@ -159,6 +161,7 @@ struct Layout {
   std::vector<uint16_t> s_pos;      // per sliced-ELL entry
   std::vector<uint16_t> tp_seg;     // n_chunks x (n_long + 1)
   int32_t tp_cap = 0;
+  int32_t s_win = 0, s_win_max = 0;  // short-chunk column window (tpl_device.h)
 };
 
 // Rows per thread of the pushed layout, or 0 when the long rows cannot be pushed:
@@ -474,6 +477,23 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
   if (L.s_width > 0)
     L.s_col16 = compress_cols(L.s_col, nchunks, (int64_t)L.s_width * kChunkRows, L.s_col16v, L.s_cbase);
   L.b_col16 = compress_cols(L.b_col, (int64_t)L.nslices * L.M, L.bin_cap, L.b_col16v, L.b_cbase);
+  // Column window of the short chunks: every chunk's columns within kWinMax of its base
+  // (uint16 columns, uniform width 1..4) -> staged in LDS (TPL_NO_WIN=1: off, experiments).
+  if (L.s_col16 && L.s_width >= 1 && L.s_width <= 4 && !(std::getenv("TPL_NO_WIN") &&
+                                                          std::getenv("TPL_NO_WIN")[0] == '1')) {
+    const int64_t per = (int64_t)L.s_width * kChunkRows;
+    int32_t win = 0, hi = 0;
+    for (int64_t c = 0; c < nchunks; ++c)
+      for (int64_t e = c * per; e < (c + 1) * per; ++e)
+        if (L.s_col[e] >= 0) {
+          win = std::max<int32_t>(win, L.s_col[e] - L.s_cbase[c] + 1);
+          hi = std::max<int32_t>(hi, L.s_col[e]);
+        }
+    if (win > 0 && win <= kWinMax) {
+      L.s_win = win;
+      L.s_win_max = hi;
+    }
+  }
   if (L.s_col16) std::vector<int32_t>().swap(L.s_col);
   if (L.b_col16) std::vector<int32_t>().swap(L.b_col);
   const int64_t g2 = (n + 1023) / 1024;
@@ -624,6 +644,8 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.push_rpt = L.push_rpt;
   A.n_comb = (A.n_long + kCombRows - 1) / kCombRows;
   A.tp_cap = L.tp_cap;
+  A.s_win = L.s_win;
+  A.s_win_max = L.s_win_max;
   A.n = op->n;
   A.E = L.E;
   return A;
