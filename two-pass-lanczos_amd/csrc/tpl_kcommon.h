@@ -20,7 +20,8 @@ namespace tpl {
 #define TPL_STAMP 0
 #endif
 #ifndef TPL_PRE_LATE
-#define TPL_PRE_LATE 0  // experiment: chunk rows' own vector entries issued after the gathers
+#define TPL_PRE_LATE 1  // chunk rows' own vector entries issued after the gathers (they are needed only
+                        // by the epilogue; issued first they delay the bins' critical loads)
 #endif
 #if TPL_STAMP
 // Diagnostic builds only: per-workgroup s_memrealtime (100 MHz) marks of the most
