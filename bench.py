@@ -52,6 +52,8 @@ def parse():
     p.add_argument("--cpu-k", type=int, default=500, help="k of the bounded CPU sample")
     p.add_argument("--cpu-reps", type=int, default=2, help="CPU sample repetitions")
     p.add_argument("--profile-iters", type=int, default=200)
+    p.add_argument("--other-configs", type=int, default=1,
+                   help="N=1: also time BASELINE configs[0] and [1] (5k inv k=50, 50k exp k=200)")
     p.add_argument("--one-pass", type=int, default=1,
                    help="N=1: also time BASELINE configs[3] (one-pass k with CGS2 "
                         "re-orthogonalisation, V_k in HBM); 0 to skip")
@@ -261,6 +263,37 @@ def main():
             "plain_one_pass_ms": round(1000 * tm[0], 3),
             "reorth_bytes": rb, "reorth_GBs": round(rate, 1),
             "reorth_frac_of_hbm": round(rate / HBM_PEAK_GBS, 4)}
+    if world == 1 and not partitioned and args.other_configs:
+        # BASELINE configs[0] and [1] on the same GPU (parity-test sizes; reported, not `value`)
+        others = {}
+        for arcs_o, k_o, f_o, ptr in ((5000, 50, "inv", _lib.FTK_INV_PTR),
+                                      (50000, 200, "exp", _lib.FTK_EXP_PTR)):
+            qf = os.path.join("/tmp", f"tpl_bench_{arcs_o}_{os.getpid()}.qfc")
+            write_qfc_3line(qf, arcs_o)
+            ko = load_kkt_system(os.path.join(ROOT, "tests", "golden", "kkt",
+                                              f"netgen-{arcs_o}-3.dmx.xz"), qf)
+            os.unlink(qf)
+            ao = ko.a
+            no = ao.shape[0]
+            opo = tpl_amd.HipCsrOp(ao, device=device)
+            bo = torch.from_numpy(ao @ np.full(no, 1.0 / np.sqrt(no))).cuda(device)
+            xo = torch.empty_like(bo)
+
+            def solve_o():
+                check(_lib.tpl_lanczos_two_pass(opo.handle, bo.data_ptr(), no, k_o, ptr, None,
+                                                xo.data_ptr(), _lib.TPL_MEM_DEVICE))
+            solve_o()
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            for _ in range(10):
+                solve_o()
+            torch.cuda.synchronize()
+            dto = (time.perf_counter() - t1) / 10
+            others[f"{arcs_o}-arc k={k_o} f={f_o}"] = {
+                "ms_per_solve": round(1000 * dto, 3), "iterations_per_s": round(k_o / dto, 1),
+                "n": no, "nnz": int(ao.nnz)}
+            opo.close()
+        out["other_configs"] = others
     if rank == 0 and args.cpu_baseline and world == 1 and not partitioned:
         import oracle  # CPU baseline only (reference-order restatement, single thread)
         from oracle import ftk_ref

@@ -5,11 +5,15 @@
 //        or dense partial-pivot LU (tests/correctness.rs:171-179) -> here: tridiagonal
 //        Gaussian elimination with partial pivoting (the LAPACK dgtsv scheme), O(k).
 //   exp: dense self-adjoint EVD, y' = Q exp(Lambda) Q^T e_1 (src/bin/stability.rs:175-193)
-//        -> here: implicit-shift QL on the tridiagonal T_k with eigenvector accumulation.
+//        -> here: implicit-shift QL on the tridiagonal T_k; Q is applied through its
+//        recorded rotations (O(k^2)) instead of being accumulated (O(k^3)).
 //   sq : y' = T_k^2 e_1 (tests/correctness.rs:287-299).
-// All three are O(k) or O(k^3) host work on at most 2k doubles: negligible next to
+// inv and sq are O(k), exp O(k^2) host work on at most 2k doubles: small next to
 // the 2k-1 device SpMVs of a solve.
 #include <cmath>
+#if defined(__x86_64__)
+#include <xmmintrin.h>
+#endif
 #include <cstring>
 #include <string>
 #include <vector>
@@ -17,6 +21,16 @@
 #include "tpl_internal.h"
 
 namespace {
+
+// sqrt(a^2 + b^2) without over/underflow: the plain formula when both magnitudes are
+// safely inside the double range (the usual case; glibc's hypot costs ~10x more and
+// dominates the QL sweep), std::hypot otherwise.
+inline double hyp(double a, double b) {
+  const double fa = std::fabs(a), fb = std::fabs(b);
+  const double big = fa > fb ? fa : fb, small = fa > fb ? fb : fa;
+  if (big < 1e150 && (small > 1e-150 || small == 0.0)) return std::sqrt(a * a + b * b);
+  return std::hypot(a, b);
+}
 
 void put_err(char* err, size_t cap, const std::string& m) {
   if (!err || cap == 0) return;
@@ -106,11 +120,32 @@ int tpl_ftk_exp(const double* alphas, size_t n_alphas, const double* betas, size
     put_err(err_msg, err_cap, "inconsistent tridiagonal sizes");
     return 1;
   }
-  // Implicit QL with Wilkinson-type shifts (tql2 scheme). z is column-major n x n,
-  // column i = eigenvector i.
-  std::vector<double> d(alphas, alphas + n), e(n, 0.0), z(n * n, 0.0);
+  // The converged off-diagonals and the first-row entries of converged eigenvectors
+  // decay into the subnormal range, where every x86 operation costs ~100 cycles (73 ns
+  // per rotation at k = 200); subnormals are flushed to zero for this solve only (their
+  // contribution to y' is below 1e-300 relative) and the caller's mode is restored.
+#if defined(__x86_64__)
+  struct FtzGuard {
+    unsigned int saved = _mm_getcsr();
+    FtzGuard() { _mm_setcsr(saved | 0x8040); }  // FTZ | DAZ
+    ~FtzGuard() { _mm_setcsr(saved); }
+  } ftz;
+#endif
+  // Implicit QL with Wilkinson-type shifts (tql2 scheme), O(k^2): instead of
+  // accumulating the eigenvector matrix Q = R_1 R_2 ... R_m (O(k) work per rotation), keep
+  // only its first row q0 (u = Q^T e_1) and the rotations themselves; then
+  // y' = Q exp(Lambda) Q^T e_1 = R_1 (R_2 (... (R_m w))), w_i = exp(lambda_i) q0_i.
+  std::vector<double> d(alphas, alphas + n), e(n, 0.0), q0(n, 0.0);
+  struct Rot {
+    size_t i;
+    double c, s;
+  };
+  // kept per thread across calls: a fresh multi-MB buffer per solve costs more in page
+  // faults than the QL sweep itself
+  static thread_local std::vector<Rot> rots;
+  rots.clear();
   for (size_t i = 0; i + 1 < n; ++i) e[i] = betas[i];
-  for (size_t i = 0; i < n; ++i) z[i * n + i] = 1.0;
+  q0[0] = 1.0;
   const double eps = 2.220446049250313e-16;
   for (size_t l = 0; l < n; ++l) {
     int iter = 0;
@@ -127,7 +162,7 @@ int tpl_ftk_exp(const double* alphas, size_t n_alphas, const double* betas, size
         return 2;
       }
       double g = (d[l + 1] - d[l]) / (2.0 * e[l]);
-      double r = std::hypot(g, 1.0);
+      double r = hyp(g, 1.0);
       g = d[m] - d[l] + e[l] / (g + (g >= 0.0 ? std::fabs(r) : -std::fabs(r)));
       double s = 1.0, c = 1.0, p = 0.0;
       size_t i = m;
@@ -135,7 +170,7 @@ int tpl_ftk_exp(const double* alphas, size_t n_alphas, const double* betas, size
       while (i-- > l) {
         double f = s * e[i];
         const double bb = c * e[i];
-        r = std::hypot(f, g);
+        r = hyp(f, g);
         e[i + 1] = r;
         if (r == 0.0) {
           d[i + 1] -= p;
@@ -150,13 +185,11 @@ int tpl_ftk_exp(const double* alphas, size_t n_alphas, const double* betas, size
         p = s * r;
         d[i + 1] = g + p;
         g = c * r - bb;
-        double* zi = &z[i * n];
-        double* zi1 = &z[(i + 1) * n];
-        for (size_t kk = 0; kk < n; ++kk) {
-          f = zi1[kk];
-          zi1[kk] = s * zi[kk] + c * f;
-          zi[kk] = c * zi[kk] - s * f;
-        }
+        // Q <- Q R on columns (i, i+1): only row 0 is kept, the rotation is recorded
+        f = q0[i + 1];
+        q0[i + 1] = s * q0[i] + c * f;
+        q0[i] = c * q0[i] - s * f;
+        rots.push_back(Rot{i, c, s});
       }
       if (early) continue;
       d[l] -= p;
@@ -164,12 +197,12 @@ int tpl_ftk_exp(const double* alphas, size_t n_alphas, const double* betas, size
       e[m] = 0.0;
     }
   }
-  // y'_r = sum_i Q[r,i] exp(lambda_i) Q[0,i]
-  for (size_t r = 0; r < n; ++r) y_out[r] = 0.0;
-  for (size_t i = 0; i < n; ++i) {
-    const double* q = &z[i * n];
-    const double w = std::exp(d[i]) * q[0];
-    for (size_t r = 0; r < n; ++r) y_out[r] += q[r] * w;
+  for (size_t i = 0; i < n; ++i) y_out[i] = std::exp(d[i]) * q0[i];
+  for (size_t t = rots.size(); t-- > 0;) {  // y' = R_1 (... (R_m w))
+    const Rot& R = rots[t];
+    const double a = y_out[R.i], b = y_out[R.i + 1];
+    y_out[R.i] = R.c * a + R.s * b;
+    y_out[R.i + 1] = -R.s * a + R.c * b;
   }
   return 0;
 }
