@@ -19,14 +19,17 @@ with open(os.path.join(out, "bench.log")) as f:
     line = [l for l in f if l.startswith("{")][-1]
 with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
     f.write(line)
-vals, cur = {}, None
+# the headline instance of k_p2_spmv: the variant with the largest traffic (smaller
+# configs of the same bench run instantiate other template variants)
+blocks, cur = {}, None
 for l in open(os.path.join(out, "pmc_summary.txt")):
     if not l.startswith(" "):
         cur = l.strip()
         continue
     m = re.match(r"\s+(\S+)\s+([0-9.]+)", l)
     if m and cur and cur.startswith("k_p2_spmv"):
-        vals[m.group(1)] = float(m.group(2))
+        blocks.setdefault(cur, {})[m.group(1)] = float(m.group(2))
+vals = max(blocks.values(), key=lambda v: v.get("FETCH_SIZE", 0.0))
 d = {"kernel": "k_p2_spmv", "config": "500k-arc KKT, lanczos_two_pass k=500 (bench.py --steps 1 --warmup 0)",
      "FETCH_SIZE_KiB": vals["FETCH_SIZE"], "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
      "traffic_bytes_per_launch": round(2 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024),

@@ -485,12 +485,13 @@ static inline size_t spmv_lds_bytes(const CsrDev& A) {
       TPL_LAUNCH_CASE(KERNEL, 89); TPL_LAUNCH_CASE(KERNEL, 90); TPL_LAUNCH_CASE(KERNEL, 91); TPL_LAUNCH_CASE(KERNEL, 92);\
       TPL_LAUNCH_CASE(KERNEL, 113); TPL_LAUNCH_CASE(KERNEL, 114); TPL_LAUNCH_CASE(KERNEL, 115); TPL_LAUNCH_CASE(KERNEL, 116);\
       TPL_LAUNCH_CASE(KERNEL, 121); TPL_LAUNCH_CASE(KERNEL, 122); TPL_LAUNCH_CASE(KERNEL, 123); TPL_LAUNCH_CASE(KERNEL, 124);\
-      default: break;                                                                   \
+      default: return hipErrorInvalidConfiguration; /* no instance for this layout */    \
     }                                                                                       \
+    return hipGetLastError();                                                               \
   }(__VA_ARGS__)
 
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s) {
-  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_spmv, A, s, A, x, y);
+  if (spmv_grid(A) > 0) return TPL_LAUNCH_CW(k_spmv, A, s, A, x, y);
   return hipGetLastError();
 }
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s) {
@@ -499,7 +500,8 @@ hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStrea
 }
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
-  if (spmv_grid(A) > 0) TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
+  if (spmv_grid(A) > 0)
+    return TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
@@ -516,7 +518,7 @@ hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
                    int nflush, hipStream_t s) {
   if (spmv_grid(A) > 0)
-    TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j, nflush);
+    return TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j, nflush);
   return hipGetLastError();
 }
 int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kLongEpiRows; }
