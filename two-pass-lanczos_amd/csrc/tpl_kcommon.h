@@ -481,6 +481,9 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                          const double* __restrict__ xsrc, ScaleFn scale_of,
                                          const Epi& epi, double* lds) {
   const int t = threadIdx.x;
+#ifdef TPL_BIN_PRIO
+  __builtin_amdgcn_s_setprio(TPL_BIN_PRIO);  // experiment: bins are the critical path
+#endif
   const int bin = __builtin_amdgcn_readfirstlane(m * A.n_slices + s);  // scalar loads below
   const int base = bin * A.bin_cap;
   const int cbase = C16 ? A.b_cbase[bin] : 0;
