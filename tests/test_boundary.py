@@ -116,6 +116,8 @@ def _tridiags(rng):
     yield np.zeros(6), rng.uniform(0.5, 2.0, 5)                # KKT-like: zero diagonal, even k
     yield rng.standard_normal(40), rng.uniform(0.1, 3.0, 39)
     yield -np.abs(rng.standard_normal(200)) * 10, rng.uniform(0.1, 3.0, 199)
+    yield np.zeros(500), rng.uniform(0.1, 1.0, 499)           # KKT-like at the headline k
+    yield rng.standard_normal(7), rng.uniform(0.1, 3.0, 6)     # smaller after larger (exp reuses its buffers)
 
 
 @pytest.mark.parametrize("name", ["inv", "exp", "sq"])
