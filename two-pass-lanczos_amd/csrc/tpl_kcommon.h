@@ -249,6 +249,9 @@ __device__ __forceinline__ void p2_epi_ptrs(EpiPass2& epi, const double* v_cur, 
   epi.v_cur = v_cur;
   epi.v_prev = (j >= 2) ? v_prev : v_cur;
   epi.has_prev = j >= 2;
+#ifdef TPL_NO_X
+  nflush = 0;  // timing experiment only: no solution updates (wrong x)
+#endif
   epi.nflush = nflush;
   epi.v_next = v_next;
   epi.x = x;
