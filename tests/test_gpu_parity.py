@@ -458,3 +458,27 @@ def test_int8_value_format_bitwise(kkt_tmp):
     assert np.array_equal(d8.alphas, d64.alphas) and np.array_equal(d8.betas, d64.betas)
     op2 = tpl_amd.HipCsrOp(a * 0.5)
     assert not op2.int8_values
+
+
+def test_synthetic_generator_instance_bitwise():
+    """BASELINE configs[4]'s instance family (tpl_generate_kkt, the 5M-arc multi-GPU
+    workload) at 200k arcs on one GPU: the layout rules that apply at that size
+    (4 column slices, chunk window) against the oracle, bit for bit; run to run equal."""
+    from tpl_amd.utils.data_loader import generate_kkt
+    a = generate_kkt(200000, seed=42).a
+    n = a.shape[0]
+    b = harness_b(a)
+    op = HipCsrOp(a)
+    sch = op.schedule()
+    assert sch["slices"] == canon_schedule(a)["slices"]
+    o = canon(op, a)
+    k = 80
+    d = alg.lanczos_pass_one(op, b, k)
+    al, be, st, bn, _ = o.pass_one(b, k)
+    assert d.steps_taken == st and d.b_norm == bn
+    assert np.array_equal(d.alphas, al) and np.array_equal(d.betas, be)
+    x = solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    assert np.array_equal(x, o.lanczos_two_pass(b, k, ftk.INV))
+    assert np.array_equal(x, solvers.lanczos_two_pass(op, b, k, ftk.INV))
+    assert n == a.shape[1]
+    op.close()
