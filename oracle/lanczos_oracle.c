@@ -94,8 +94,8 @@ static void spmv_faithful(const ocsr* A, const double* x, double* y) {
 
 /* long row: per slice s (columns [floor(n*s/S), floor(n*(s+1)/S))) the slice's entries
  * form a piece; a piece of at most BIG_PIECE entries: lane g (0..7) sums its entries
- * g + 8q, butterfly over the 8 lanes (xor 1, 2, 4); a longer piece: lane l (0..63) sums
- * its entries l + 64q, tree64. -> P_s; y = 0; y += P_s (s ascending). S: the
+ * g + 8q, butterfly over the 8 lanes (xor 1, 2, 4); a longer piece: lane g (0..15) sums
+ * its entries g + 16q, butterfly over 16 lanes. -> P_s; y = 0; y += P_s (s ascending). S: the
  * schedule's slice count (tpl_runtime.cpp auto_slices).
  * (device: long_bin in tpl_kernels.hip; kBigPiece in tpl_device.h) */
 #define BIG_PIECE 64
@@ -107,23 +107,18 @@ static double long_row_canon(const ocsr* A, int32_t i, const double* x, int S) {
     const int64_t bound = (s + 1 == S) ? INT64_MAX : n * (s + 1) / S;
     int64_t e = q;
     while (e < A->rp[i + 1] && A->ci[e] < bound) ++e;
-    const int G = (e - q > BIG_PIECE) ? 64 : 8;
-    double lane[64], nx[64];
+    const int G = (e - q > BIG_PIECE) ? 16 : 8;
+    double lane[16], nx[16];
     for (int g = 0; g < G; ++g) {
       double p = 0.0;
       for (int64_t k = q + g; k < e; k += G) p = p + A->v[k] * x[A->ci[k]];
       lane[g] = p;
     }
-    double ps;
-    if (G == 64) {
-      ps = tree64(lane);
-    } else {
-      for (int h = 1; h < 8; h <<= 1) {
-        for (int g = 0; g < 8; ++g) nx[g] = lane[g] + lane[g ^ h];
-        memcpy(lane, nx, 8 * sizeof(double));
-      }
-      ps = lane[0];
+    for (int h = 1; h < G; h <<= 1) {
+      for (int g = 0; g < G; ++g) nx[g] = lane[g] + lane[g ^ h];
+      memcpy(lane, nx, (size_t)G * sizeof(double));
     }
+    const double ps = lane[0];
     y = y + ps;
     q = e;
   }

@@ -37,8 +37,8 @@
 //   * long row         : per slice s, its L entries form a piece. L <= kBigPiece: lane
 //                        g (0..7): p_g = 0; p_g += round(a_k x_k) for the piece's
 //                        entries k = g + 8q (q ascending); P_s = xor butterfly of p over
-//                        8 lanes (offsets 1, 2, 4). L > kBigPiece: the same with 64
-//                        lanes (k = g + 64q) and the 64-lane butterfly of tree256.
+//                        8 lanes (offsets 1, 2, 4). L > kBigPiece: the same with 16
+//                        lanes (k = g + 16q) and a 16-lane butterfly (1, 2, 4, 8).
 //                        y = 0; y += P_s, s = 0..S-1.
 //   * long row, pushed : chunk w (positions [Cw, C(w+1)), C = 512 * push_rpt): the
 //                        row's entries in the chunk's short rows, ascending, are a run
@@ -71,7 +71,7 @@ constexpr int kRowsPerThread = kChunkRows / kTPB;
 constexpr int kShortRowMax = 32;     // upper bound of the short-row threshold
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
 constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB table slots)
-// Pieces longer than this are summed by a whole wave (64 lanes), the others by 8 lanes;
+// Pieces longer than this are summed by 16 lanes, the others by 8 lanes;
 // the long pieces of a bin come first in its table (CsrDev::b_hdr holds their count).
 constexpr int kBigPiece = 64;
 #ifndef TPL_BIN_MIN

@@ -84,6 +84,15 @@ __device__ __forceinline__ double group8_sum(double v) {
   return v;
 }
 
+// Sum over each aligned group of 16 lanes (butterfly offsets 1, 2, 4, 8), all on DPP.
+__device__ __forceinline__ double group16_sum(double v) {
+  v = v + dpp_f64<0xB1>(v);   // xor 1
+  v = v + dpp_f64<0x4E>(v);   // xor 2
+  v = v + dpp_f64<0x141>(v);  // partner quad in the 8-lane group
+  v = v + dpp_f64<0x140>(v);  // partner 8-lane group in the 16-lane row
+  return v;
+}
+
 // tree256; every thread returns the block total. red: 4 doubles of LDS.
 __device__ __forceinline__ double block_sum(double v, double* red) {
   v = wave_sum(v);
@@ -534,24 +543,29 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   starts[t] = sg.ri < 0 ? -1 - sg.start : sg.start;  // < 0: no piece (value encodes the fill)
   __syncthreads();
   TPL_MARK(2);
-  // Piece sums (canonical long-row order). A piece longer than kBigPiece takes a whole
-  // wave: lane l sums its entries l + 64q, then the wave butterfly. Those pieces come
-  // first in the table (nbig of them), one wave each in turn.
-  const int lane = t & 63;
+  // Piece sums (canonical long-row order). A piece longer than kBigPiece is summed by a
+  // 16-lane group — lane g sums its entries g + 16q, then the 16-lane butterfly — 16
+  // such pieces per pass (every piece of a bin at once at 500k arcs, where all pieces
+  // are long); those pieces come first in the table (nbig of them).
   if (!(TPL_ABLATE & 4)) {
-    for (int j = t >> 6; j < nbig; j += kTPB / 64) {
-      const int st = starts[j], nx = starts[j + 1];
-      const int en = nx >= 0 ? nx : -1 - nx;
+    const int g16 = t & 15;
+    for (int j0 = 0; j0 < nbig; j0 += kTPB / 16) {
+      const int j = j0 + (t >> 4);
+      const bool valid = j < nbig;
+      const int jc = valid ? j : 0;
+      const int st = starts[jc], nx = starts[jc + 1];
+      const int b0 = valid ? st : 0;
+      const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
       double acc = 0.0;
-      for (int k0 = st + lane; k0 < en; k0 += 512) {  // 8 reads in flight, then the adds
+      for (int k0 = b0 + g16; k0 < en; k0 += 128) {  // 8 reads in flight, then the adds
         double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 64 * u < en ? k0 + 64 * u : k0];
+        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 16 * u < en ? k0 + 16 * u : k0];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = k0 + 64 * u < en ? acc + v[u] : acc;
+        for (int u = 0; u < 8; ++u) acc = k0 + 16 * u < en ? acc + v[u] : acc;
       }
-      acc = wave_sum(acc);
-      if (lane == 0) psum[j] = acc;
+      acc = group16_sum(acc);
+      if (g16 == 0 && valid) psum[j] = acc;
     }
   }
   // The other pieces, 32 per pass: the 8-lane group t >> 3 takes one; its lane g sums

@@ -32,15 +32,6 @@
 
 namespace tpl {
 
-// Sum over each aligned group of 16 lanes (butterfly offsets 1, 2, 4, 8), all on DPP.
-__device__ __forceinline__ double group16_sum(double v) {
-  v = v + dpp_f64<0xB1>(v);   // xor 1
-  v = v + dpp_f64<0x4E>(v);   // xor 2
-  v = v + dpp_f64<0x141>(v);  // partner quad in the 8-lane group
-  v = v + dpp_f64<0x140>(v);  // partner 8-lane group in the 16-lane row
-  return v;
-}
-
 // partials() (tpl_device.h) in a workgroup of kPushTPB threads: threads 0..255 follow
 // the canonical 256-thread order (tree256), the others contribute nothing.
 __device__ __forceinline__ double finish_partials_256(const double* __restrict__ P, int N,
