@@ -4,8 +4,9 @@ import os, sys, json, subprocess
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if os.environ.get("TPL_CHILD") != "1":
     libs = json.loads(os.environ.get("LIBS", "[\"\"]"))
-    for lib in libs:
-        env = dict(os.environ, TPL_CHILD="1")
+    for spec in libs:  # "path[;KEY=VALUE...]"
+        lib, *kv = spec.split(";")
+        env = dict(os.environ, TPL_CHILD="1", **dict(x.split("=", 1) for x in kv))
         if lib:
             env["TPL_LIB_PATH"] = lib
         subprocess.run([sys.executable, __file__], env=env, check=False)
@@ -23,7 +24,7 @@ op = tpl_amd.HipCsrOp(a)
 op.set_slices(int(os.environ.get("SLICES", "0")))
 op.set_push(os.environ.get("PUSH", "0") == "1")
 tpl_amd.lanczos_two_pass(op, b, 50, "inv")
-row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "slices": op.schedule()["slices"], "push": op.pushed}
+row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "own": os.environ.get("TPL_OWNER_SLICES", ""), "slices": op.schedule()["slices"], "push": op.pushed}
 if os.environ.get("SOLVE", "1") == "1":  # full two-pass k=500 solves (ms, best of 5)
     import time
     tpl_amd.lanczos_two_pass(op, b, 500, "inv")

@@ -18,6 +18,8 @@ for p in (ROOT, os.path.join(ROOT, "two-pass-lanczos_amd")):
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 KKT_DIR = os.path.join(GOLDEN, "kkt")
 REF_RESULTS = os.path.join(GOLDEN, "reference_results")
+ELEM_ROWS = 2048   # kElemRows (two-pass-lanczos_amd/csrc/tpl_device.h): rows per element-wise block
+CHUNK_ROWS = 512   # kChunkRows
 
 # md5 of the decompressed netgen .dmx files (regenerated from the reference's own
 # netgen sources + recorded .par seeds; tests/golden/make_fixtures.py)
@@ -103,7 +105,7 @@ def canon_schedule(a, short_row_max=-1, max_g2=1024, push=False):
     T = short_row_threshold(lens, short_row_max)
     short = np.nonzero(lens <= T)[0].astype(np.int32)
     long_ = np.nonzero(lens > T)[0].astype(np.int32)
-    g2 = max(1, min(max_g2, -(-n // 1024)))
+    g2 = max(1, min(max_g2, -(-n // ELEM_ROWS)))
     per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)
     rpt = 0

@@ -68,6 +68,15 @@ constexpr int kTPB = 256;            // threads per workgroup (4 waves of 64)
 #endif
 constexpr int kChunkRows = TPL_CHUNK_ROWS; // short-row positions per SELL chunk
 constexpr int kRowsPerThread = kChunkRows / kTPB;
+#ifndef TPL_ELEM_ROWS
+#define TPL_ELEM_ROWS 2048
+#endif
+// rows per workgroup of the element-wise kernels (k_p1_axpy, ...): G2 = ceil(n / this)
+// workgroups, a multiple of kChunkRows (chunk_of_block keeps a chunk on its element
+// block's XCD). 2048 at 500k arcs: k_p1_axpy 3.97 us vs 4.24 at 1024 (each workgroup
+// re-reduces the ~2.1k alpha partials; fewer workgroups, less of that), 4.94 at 4096
+// (too few workgroups to stream); solve 12.58 vs 12.69 ms.
+constexpr int kElemRows = TPL_ELEM_ROWS;
 constexpr int kShortRowMax = 32;     // upper bound of the short-row threshold
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
 constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB table slots)

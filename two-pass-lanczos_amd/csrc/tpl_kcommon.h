@@ -144,6 +144,9 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
 #ifndef TPL_WT_W
 #define TPL_WT_W 1  // pass one's w (read next by k_p1_axpy on the same XCD only)
 #endif
+#ifndef TPL_WT_V
+#define TPL_WT_V 1  // pass two's v_{j+1} (gathered by every XCD next step)
+#endif
 #ifndef TPL_WT_X
 #define TPL_WT_X 1  // pass two's x (read again three steps later, same XCD only)
 #endif
@@ -235,7 +238,11 @@ struct EpiPass2 {
     double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
+#if TPL_WT_V
     st_out(v_next + i, vn);
+#else
+    st_plain(v_next + i, vn);
+#endif
     if (nflush) {
       double xv = p.x;
       if (nflush >= 3) xv = xv + ycoef2 * p.vp;
@@ -647,13 +654,15 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
 // on XCD 0, scripts/lab/xcd_rr.hip), and an XCD's L2 keeps the lines a kernel wrote
 // there for the next kernel (scripts/lab/l2_keep.hip: 32 MB re-read 7.4 us on the
 // writing XCD vs 10.4 us elsewhere). Short chunk c (512 rows) lies in element-wise block
-// c / 2 (E = 1024 rows), which k_p1_axpy / k_p1_init run on XCD (c / 2) % 8; the chunk
-// part of an SpMV grid (padded to a multiple of 16) places chunk c = 16q + 2x + e on a
-// block of XCD x, so the rows' vectors (r, w, v, x) stay in one XCD's L2 from launch
-// to launch. i: block index within the chunk part; returns -1 for padding blocks.
+// c / cpe (cpe = kElemRows / kChunkRows chunks per block), which k_p1_axpy / k_p1_init
+// run on XCD (c / cpe) % 8; the chunk part of an SpMV grid (padded to a multiple of
+// 8 cpe) places chunk c = 8 cpe q + cpe x + e on a block of XCD x, so the rows' vectors
+// (r, w, v, x) stay in one XCD's L2 from launch to launch. i: block index within the
+// chunk part; -1 for padding blocks.
 __device__ __forceinline__ int chunk_of_block(const CsrDev& A, int i) {
+  constexpr int cpe = kElemRows / kChunkRows;  // chunks per element-wise block
   const int x = ((i & 7) + A.n_slice_blocks) & 7;
-  const int c = (i >> 4) * 16 + 2 * x + ((i >> 3) & 1);
+  const int c = (i / (8 * cpe)) * (8 * cpe) + cpe * x + ((i >> 3) % cpe);
   return c < A.n_chunks ? c : -1;
 }
 

@@ -137,7 +137,8 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                "s"(S.norms), "s"(S.alphas), "s"(S.Pb));
   asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k));
   PartialRegs<12> pr;
-  load_partials(S.Pa_r, A.NA_r, pr);
+  const int na_ = A.NA_r;
+  load_partials(S.Pa_r, na_, pr);
   const int64_t beg = (int64_t)blockIdx.x * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
   // All of this thread's pairs (up to kAxPairs) are loaded before alpha is known, at
@@ -164,7 +165,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     keep(w0[q].x); keep(w0[q].y); keep(rc0[q].x); keep(rc0[q].y);
   }
   if (stop) return;
-  const double alpha = finish_partials(S.Pa_r, A.NA_r, pr, red);
+  const double alpha = finish_partials(S.Pa_r, na_, pr, red);
   if (blockIdx.x == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
@@ -449,8 +450,11 @@ static inline int elem_grid(int64_t n) {
   if (g < 1) g = 1;
   return (int)g;
 }
-// chunk part padded to a multiple of 16 (chunk_of_block in tpl_kcommon.h)
-static inline int spmv_grid(const CsrDev& A) { return A.n_slice_blocks + (A.n_chunks + 15) / 16 * 16; }
+// chunk part padded to a multiple of 8 x chunks per element block (chunk_of_block)
+static inline int spmv_grid(const CsrDev& A) {
+  constexpr int g = 8 * (kElemRows / kChunkRows);
+  return A.n_slice_blocks + (A.n_chunks + g - 1) / g * g;
+}
 // dynamic LDS of the SpMV-shaped kernels: a bin's staged products + piece starts
 static inline size_t spmv_lds_bytes(const CsrDev& A) {
   const size_t bins = A.n_slice_blocks > 0

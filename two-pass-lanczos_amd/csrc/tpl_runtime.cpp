@@ -496,7 +496,7 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
   }
   if (L.s_col16) std::vector<int32_t>().swap(L.s_col);
   if (L.b_col16) std::vector<int32_t>().swap(L.b_col);
-  const int64_t g2 = (n + 1023) / 1024;
+  const int64_t g2 = (n + kElemRows - 1) / kElemRows;
   L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
   const int64_t per = (n + L.G2 - 1) / L.G2;
   L.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
