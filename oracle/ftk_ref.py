@@ -43,8 +43,14 @@ def exp(alphas, betas) -> np.ndarray:
         return np.zeros(0)
     if k == 1:
         return np.array([np.exp(float(alphas[0]))])
-    lam, q = eigh_tridiagonal(np.asarray(alphas, dtype=np.float64),
-                              np.asarray(betas[:k - 1], dtype=np.float64))
+    d = np.asarray(alphas, dtype=np.float64)
+    e = np.asarray(betas[:k - 1], dtype=np.float64)
+    try:
+        lam, q = eigh_tridiagonal(d, e)
+    except np.linalg.LinAlgError:
+        # dstemr (MRRR) gives up on some large zero-diagonal KKT projections (k = 500
+        # on the 500k instance); implicit QL/QR (dstev) is the classical fallback
+        lam, q = eigh_tridiagonal(d, e, lapack_driver="stev")
     return q @ (np.exp(lam) * q[0, :])
 
 

@@ -30,6 +30,9 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
 
 #define TPB 256
 #define TOL 2.220446049250313080847263336181640625e-13 /* 1000 * f64::EPSILON */
@@ -37,11 +40,15 @@
 enum { OR_OK = 0, OR_ZERO_B = 3, OR_BAD = 100 };
 
 typedef struct {
-  int64_t n;
+  int64_t n;             /* rows */
   const int64_t* rp;
   const int32_t* ci;
   const double* v;
+  int64_t ncols;         /* columns (<= 0: square); a rank's row block of a partition has
+                          * n_global columns, and the long-row slices split those */
 } ocsr;
+
+static int64_t ncols_of(const ocsr* A) { return A->ncols > 0 ? A->ncols : A->n; }
 
 typedef struct {
   int32_t n_short;
@@ -59,11 +66,11 @@ typedef struct {
 
 /* ------------------------------------------------------------ trees */
 static double tree64(double* a) { /* xor butterfly, offsets 1, 2, 4, 8, 16, 32 */
-  double nx[64];
-  for (int h = 1; h < 64; h <<= 1) {
-    for (int l = 0; l < 64; ++l) nx[l] = a[l] + a[l ^ h];
-    memcpy(a, nx, sizeof(nx));
-  }
+  /* lane 0's value after stage h only needs the lanes l = 0 mod 2h, and for those
+   * l ^ h == l + h: the butterfly's lane 0 is this in-place pairwise tree (addition
+   * is commutative, so a_l + a_{l^h} is the same bits for either operand order) */
+  for (int h = 1; h < 64; h <<= 1)
+    for (int l = 0; l < 64; l += 2 * h) a[l] = a[l] + a[l + h];
   return a[0];
 }
 static double tree256(const double* a) {
@@ -85,6 +92,7 @@ static double reduce_partials(const double* P, int G) {
 
 /* ------------------------------------------------------------ SpMV */
 static void spmv_faithful(const ocsr* A, const double* x, double* y) {
+  #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < A->n; ++i) {
     double s = 0.0;
     for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
@@ -100,7 +108,7 @@ static void spmv_faithful(const ocsr* A, const double* x, double* y) {
  * (device: long_bin in tpl_kernels.hip; kBigPiece in tpl_device.h) */
 #define BIG_PIECE 64
 static double long_row_canon(const ocsr* A, int32_t i, const double* x, int S) {
-  const int64_t n = A->n;
+  const int64_t n = ncols_of(A);
   int64_t q = A->rp[i];
   double y = 0.0;
   for (int s = 0; s < S; ++s) {
@@ -177,6 +185,7 @@ static double long_row_push(const ocsr* A, const osched* S, int32_t i, const dou
 }
 
 static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* y) {
+  #pragma omp parallel for schedule(static)
   for (int32_t p = 0; p < S->n_short; ++p) {
     const int32_t i = S->srows[p];
     double s = 0.0;
@@ -184,15 +193,16 @@ static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* 
     y[i] = s;
   }
   if (S->push && S->n_long > 0) {
-    int32_t* pos = (int32_t*)malloc(sizeof(int32_t) * (size_t)(A->n + 1));
+    int32_t* pos = (int32_t*)malloc(sizeof(int32_t) * (size_t)(ncols_of(A) + 1));
     double* P = (double*)malloc(sizeof(double) * (size_t)(S->n_short / chunk_rows(S) + 2));
-    for (int64_t c = 0; c < A->n; ++c) pos[c] = -1;
+    for (int64_t c = 0; c < ncols_of(A); ++c) pos[c] = -1;
     for (int32_t p = 0; p < S->n_short; ++p) pos[S->srows[p]] = p;
     for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_push(A, S, S->lrows[r], x, pos, P);
     free(pos);
     free(P);
     return;
   }
+  #pragma omp parallel for schedule(static)
   for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_canon(A, S->lrows[r], x, S->slices);
 }
 
@@ -208,11 +218,12 @@ static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
  * ((S4+S5)+(S6+S7)) of the 8 wave butterflies); long row r -> partial n_chunks + r =
  * round(v * w); then reduce_partials over all of them. */
 static double dot_canon(const osched* S, const double* v, const double* w, double* P) {
-  double acc[2 * TPB];
   const int NT = S->push ? 2 * TPB : TPB;
   const int32_t C = chunk_rows(S);
   const int32_t nch = (S->n_short + C - 1) / C;
+#pragma omp parallel for schedule(static)
   for (int32_t c = 0; c < nch; ++c) {
+    double acc[2 * TPB];
     for (int t = 0; t < NT; ++t) {
       acc[t] = 0.0;
       for (int q = 0; q < C / NT; ++q) {
@@ -233,8 +244,9 @@ static double dot_faithful(int64_t n, const double* v, const double* w) {
 
 /* ||x||^2: device order = E-partition, thread t visits pairs bE + 2t + 512q. */
 static double nrm2_canon(const osched* S, int64_t n, const double* x, double* P) {
-  double acc[TPB];
+#pragma omp parallel for schedule(static)
   for (int b = 0; b < S->G2; ++b) {
+    double acc[TPB];
     const int64_t beg = (int64_t)b * S->E;
     const int64_t end = beg + S->E < n ? beg + S->E : n;
     for (int t = 0; t < TPB; ++t) {
@@ -264,22 +276,25 @@ static double nrm2_faithful(int64_t n, const double* x) {
  * re-orthogonalisation; pinned only against this restatement and orthonormality.) */
 static void reorth_canon(const osched* S, int64_t n, const double* V, int cols, double* r,
                          double* P, double* h) {
-  double acc[TPB];
   for (int pass = 0; pass < 2; ++pass) {
-    for (int c = 0; c < cols; ++c) {
-      const double* col = V + (size_t)c * (size_t)n;
-      for (int b = 0; b < S->G2; ++b) {
-        const int64_t beg = (int64_t)b * S->E;
-        const int64_t end = beg + S->E < n ? beg + S->E : n;
+    /* P[c * G2 + b]: the (column, workgroup) trees; workgroups are independent */
+#pragma omp parallel for schedule(static)
+    for (int b = 0; b < S->G2; ++b) {
+      double acc[TPB];
+      const int64_t beg = (int64_t)b * S->E;
+      const int64_t end = beg + S->E < n ? beg + S->E : n;
+      for (int c = 0; c < cols; ++c) {
+        const double* col = V + (size_t)c * (size_t)n;
         for (int t = 0; t < TPB; ++t) {
           double a = 0.0;
           for (int64_t i = beg + t; i < end; i += TPB) a = fma(col[i], r[i], a);
           acc[t] = a;
         }
-        P[b] = tree256(acc);
+        P[(size_t)c * (size_t)S->G2 + (size_t)b] = tree256(acc);
       }
-      h[c] = reduce_partials(P, S->G2);
     }
+    for (int c = 0; c < cols; ++c) h[c] = reduce_partials(P + (size_t)c * (size_t)S->G2, S->G2);
+#pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) {
       double sum = 0.0;
       for (int c = 0; c < cols; ++c) sum = fma(V[(size_t)c * (size_t)n + i], h[c], sum);
@@ -297,8 +312,8 @@ static int pass_one_impl(const ocsr* A, const osched* S, const double* b, size_t
   if (k == 0) return OR_BAD;
   if (reorth && (!S || !V)) return OR_BAD;
   double* h = reorth ? (double*)malloc(sizeof(double) * k) : NULL;
-  double* P = S ? (double*)malloc(sizeof(double) * (size_t)(S->n_short + S->n_long + S->G2 + 1))
-                : NULL;
+  const size_t np = S ? (size_t)(S->n_short + S->n_long + S->G2 + 1) : 0;
+  double* P = S ? (double*)malloc(sizeof(double) * (reorth ? np + (size_t)S->G2 * k : np)) : NULL;
   double* vp = (double*)calloc((size_t)n + 1, sizeof(double));
   double* vc = (double*)malloc(sizeof(double) * ((size_t)n + 1));
   double* w = (double*)malloc(sizeof(double) * ((size_t)n + 1));
@@ -310,23 +325,27 @@ static int pass_one_impl(const ocsr* A, const osched* S, const double* b, size_t
     return OR_ZERO_B;
   }
   const double inv0 = 1.0 / bnorm;
+  #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) vc[i] = b[i] * inv0;
   double beta_prev = 0.0;
   size_t nb = 0;
   for (size_t it = 0; it < k; ++it) {
     if (V) memcpy(V + it * (size_t)n, vc, sizeof(double) * (size_t)n);
     spmv(A, S, vc, w);                                                /* :177 */
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] - beta_prev * vp[i]; /* :184-186 */
     const double alpha = S ? dot_canon(S, vc, w, P) : dot_faithful(n, vc, w); /* :191 */
     alphas[it] = alpha;
     *steps = it + 1;
     if (it + 1 == k) break; /* beta_k is never used */
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] - alpha * vc[i];     /* :196-198 */
     if (reorth) reorth_canon(S, n, V, (int)(it + 1), w, P, h);        /* extension */
     const double beta = sqrt(S ? nrm2_canon(S, n, w, P) : nrm2_faithful(n, w)); /* :202 */
     if (beta <= TOL) break;                                           /* :206-208 */
     betas[nb++] = beta;
     const double inv = 1.0 / beta;                                    /* :312-315 */
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] * inv;
     double* t = vp;
     vp = vc;
@@ -362,17 +381,23 @@ int oracle_pass_two(const ocsr* A, const osched* S, const double* b, const doubl
   double* vc = (double*)malloc(sizeof(double) * ((size_t)n + 1));
   double* w = (double*)malloc(sizeof(double) * ((size_t)n + 1));
   const double inv0 = 1.0 / bnorm;
+  #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) vc[i] = b[i] * inv0;
+  #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) x[i] = vc[i] * y[0];
   if (V) memcpy(V, vc, sizeof(double) * (size_t)n);
   for (size_t j = 0; j + 1 < steps; ++j) {
     const double alpha = alphas[j], beta = betas[j], beta_prev = j == 0 ? 0.0 : betas[j - 1];
     spmv(A, S, vc, w);
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] - beta_prev * vp[i];
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] - alpha * vc[i];
     const double inv = 1.0 / beta;
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] * inv;
     const double c = y[j + 1];
+    #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) x[i] = x[i] + c * w[i];
     double* t = vp;
     vp = vc;
@@ -387,6 +412,7 @@ int oracle_pass_two(const ocsr* A, const osched* S, const double* b, const doubl
 /* x = ||b|| (V y'): canonical = per row fma chain over columns, then scale. */
 void oracle_gemv_recon(int64_t n, size_t steps, const double* V, const double* yprime,
                        double bnorm, double* x, int canonical) {
+  #pragma omp parallel for schedule(static)
   for (int64_t i = 0; i < n; ++i) {
     double s = 0.0;
     if (canonical)
@@ -397,7 +423,54 @@ void oracle_gemv_recon(int64_t n, size_t steps, const double* V, const double* y
   }
 }
 
+/* Threads of the row / block / element loops (results do not depend on it: every
+ * parallel loop writes independent rows, partials or elements). bench.py's CPU
+ * baseline sets 1 (the reference is single-threaded, Par::Seq). */
+void oracle_set_threads(int t) {
+#ifdef _OPENMP
+  omp_set_num_threads(t > 0 ? t : 1);
+#else
+  (void)t;
+#endif
+}
+
 void oracle_spmv(const ocsr* A, const osched* S, const double* x, double* y) { spmv(A, S, x, y); }
+
+/* Building blocks of the partitioned orders (tests/partition_oracle.py composes them):
+ * alpha partial total v . w of one operator's rows (device order, or sequential without
+ * a schedule), sum of squares (no sqrt), partials() of an array, and the replicated long
+ * rows' alpha partials (k_long_epi_p1: blocks of 1024 long rows, thread t accumulates
+ * fma(v, w) over rows t + 256 q, tree256). */
+double oracle_dot(const osched* S, int64_t n, const double* v, const double* w) {
+  if (!S) return dot_faithful(n, v, w);
+  double* P = (double*)malloc(sizeof(double) * (size_t)(S->n_short + S->n_long + 1));
+  const double r = dot_canon(S, v, w, P);
+  free(P);
+  return r;
+}
+double oracle_sumsq(const osched* S, int64_t n, const double* x) {
+  if (!S) return nrm2_faithful(n, x);
+  double* P = (double*)malloc(sizeof(double) * (size_t)(S->G2 + 1));
+  const double r = nrm2_canon(S, n, x, P);
+  free(P);
+  return r;
+}
+double oracle_reduce(const double* P, int G) { return reduce_partials(P, G); }
+#define LONG_EPI_ROWS 1024 /* kLongEpiRows (tpl_device.h) */
+void oracle_long_alpha_blocks(int64_t nl, const double* v, const double* w, double* out) {
+  const int64_t nb = (nl + LONG_EPI_ROWS - 1) / LONG_EPI_ROWS;
+  for (int64_t b = 0; b < nb; ++b) {
+    double acc[TPB];
+    const int64_t l0 = b * LONG_EPI_ROWS;
+    const int64_t l1 = l0 + LONG_EPI_ROWS < nl ? l0 + LONG_EPI_ROWS : nl;
+    for (int t = 0; t < TPB; ++t) {
+      double a = 0.0;
+      for (int64_t l = l0 + t; l < l1; l += TPB) a = fma(v[l], w[l], a);
+      acc[t] = a;
+    }
+    out[b] = tree256(acc);
+  }
+}
 
 double oracle_nrm2(const osched* S, int64_t n, const double* x) {
   if (!S) return sqrt(nrm2_faithful(n, x));

@@ -47,11 +47,19 @@ def kkt_paths(arcs: int, tmpdir: str):
 _KKT_CACHE = {}
 
 
+SYNTH_SEED = 42  # BASELINE configs[4]: tpl_generate_kkt(5_000_000, seed 42), as bench.py
+
+
 def load_kkt(arcs: int, tmpdir: str):
+    """The netgen instance of `arcs` arcs (5k / 50k / 500k fixtures), or — for any
+    other size, e.g. configs[4]'s 5M arcs — the build's synthetic generator."""
     if arcs not in _KKT_CACHE:
-        from tpl_amd.utils.data_loader import load_kkt_system
-        dmx, qfc = kkt_paths(arcs, tmpdir)
-        _KKT_CACHE[arcs] = load_kkt_system(dmx, qfc)
+        from tpl_amd.utils.data_loader import generate_kkt, load_kkt_system
+        if arcs in KKT_MD5:
+            dmx, qfc = kkt_paths(arcs, tmpdir)
+            _KKT_CACHE[arcs] = load_kkt_system(dmx, qfc)
+        else:
+            _KKT_CACHE[arcs] = generate_kkt(arcs, seed=SYNTH_SEED)
     return _KKT_CACHE[arcs]
 
 

@@ -25,15 +25,20 @@ def main():
     b = harness_b(a)
     ctx = DistContext(rank, world, device=int(os.environ.get("TPL_DEVICE", "0")), transport=transport)
     op = DistHipCsrOp(a, ctx, mode=mode)
+    if os.environ.get("TPL_TEST_SLICES"):  # diagnostics: force the long-row slice count
+        op.set_slices(int(os.environ["TPL_TEST_SLICES"]))
     bl = op.local(b)
     x1 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
     x2 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
     dec = tpl_amd.algorithms.lanczos_pass_one(op, bl, k)
     xs = tpl_amd.lanczos(op, bl, k, "inv")
     y = op.apply(op.local(np.cos(np.arange(a.shape[0]))))
+    sch = op.schedule()  # this rank's layout: the partition oracle's reduction order
     np.savez(os.path.join(out, f"rank{rank}.npz"), x1=x1, x2=x2, xs=xs, y=y,
              al=dec.alphas, be=dec.betas, steps=dec.steps_taken, bn=dec.b_norm,
-             rows=op.local_rows, mode=op.mode)
+             rows=op.local_rows, mode=op.mode, s_short=sch["short_rows"],
+             s_long=sch["long_rows"], s_G2=sch["G2"], s_E=sch["E"], s_slices=sch["slices"],
+             starts=getattr(op, "starts", np.zeros(0, dtype=np.int64)))
     torch.cuda.synchronize()
     tdist.barrier()
     op.close()

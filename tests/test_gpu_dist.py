@@ -75,6 +75,21 @@ def test_one_rank_rccl_replicated(kkt_tmp, tmp_path):
     assert str(r["mode"]) == "replicated"
     xr = _assemble([r], "x1", a.shape[0])
     assert np.linalg.norm(xr - x) <= 1e-10 * np.linalg.norm(x)
+    _check_partition_order(a, [r], "replicated", 50)
+
+
+def _check_partition_order(a, rs, mode, k):
+    """alphas, betas, ||b|| and x bit for bit against the partitioned order restated on
+    the CPU (tests/partition_oracle.py)."""
+    from partition_oracle import PartitionOracle
+    import tpl_amd
+    b = harness_b(a)
+    po = PartitionOracle(a, rs, mode)
+    al, be, s, bn = po.pass_one(b, k)
+    assert int(rs[0]["steps"]) == s and float(rs[0]["bn"]) == bn
+    assert np.array_equal(rs[0]["al"], al) and np.array_equal(rs[0]["be"], be)
+    xo = po.pass_two(b, al, be, s, bn, tpl_amd.ftk.INV(al, be) * bn)
+    assert np.array_equal(_assemble(rs, "x1", a.shape[0]), xo)
 
 
 @pytest.mark.parametrize("world,mode", [(2, "rows"), (3, "rows"), (2, "replicated"),
@@ -99,6 +114,7 @@ def test_ranks_share_gpu_host_transport(kkt_tmp, tmp_path, world, mode):
             common, i0, i1 = np.intersect1d(rs[0]["rows"], r["rows"], return_indices=True)
             assert len(common) > 0
             assert np.array_equal(rs[0]["x1"][i0], r["x1"][i1])
+    _check_partition_order(a, rs, mode, 50)
     # SpMV blocks: +-1 values, exact products
     y = _assemble(rs, "y", n)
     yr = a @ np.cos(np.arange(a.shape[0]))
