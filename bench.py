@@ -3,28 +3,36 @@
 k = 500, f = inv (BASELINE.json configs[2]; metric "Lanczos iterations/sec + SpMV GB/s
 (vs HBM roofline), 500k-arc KKT k=500").
 
-A "step" = one full ``solvers::lanczos_two_pass`` call (pass one, host f(T_k) solve,
-pass two), the window the reference times (src/bin/tradeoff.rs:265-288). Inputs
-(A, b) are resident in HBM before the timed region; x stays in HBM.
+A "step" = one full ``solvers::lanczos_two_pass`` call (pass one, f(T_k) solve, pass
+two), the window the reference times (src/bin/tradeoff.rs:265-288). Inputs (A, b) are
+resident in HBM before the timed region; x stays in HBM.
 
     python bench.py [--gpus N --steps K --warmup W]
 
-N > 1 (launched by torch.distributed.run, one rank per GPU): the ranks run ONE
-row-partitioned solve of BASELINE configs[4] (5M-arc synthetic KKT, k = 500) together
-(strong scaling), timed between barriers, max over ranks; rank 0 then
-times the same workload on its GPU alone (single_gpu_same_workload).
+N > 1: when started without torch.distributed.run's environment (no WORLD_SIZE), this
+process launches ``python -m torch.distributed.run --nproc-per-node N ... bench.py`` as
+a CHILD (it never touches the GPU itself) and exits with its status. Each rank drives
+one GPU; together they run ONE row-partitioned solve of BASELINE configs[4] (5M-arc
+synthetic KKT, k = 500; strong scaling), timed between barriers, max over
+ranks; rank 0 then times the same workload on its GPU alone (single_gpu_same_workload).
+At N = 1 the line also carries that workload on one GPU (configs4_5m_1gpu), so a 1 -> N
+curve can be read on one instance. Rehearsal on a one-GPU box: TPL_DEVICE=0
+TPL_DIST_TRANSPORT=host (all ranks share GPU 0, exchanges through host memory).
 
-Extra JSON fields: ``roofline`` for the dominant kernel (algorithmic bytes per launch /
-HIP-event average launch time, vs 8 TB/s HBM3E), ``cpu_baseline`` (the oracle's
-reference-order restatement, single core, bounded sample on the host of the GPU box),
-``one_pass_reorth`` (BASELINE configs[3]: one-pass k = 500 with CGS2 re-orthogonalisation,
-its sweep rate against HBM).
+Extra JSON fields: ``roofline`` for the dominant kernel — SURVEY.md §8(d)'s B_spmv
+= 12 nnz + 4 (n+1) + 16 n per launch over the live HIP-event average launch time of
+k_p2_spmv, vs 8 TB/s (``frac``), with the fused-epilogue byte count, pass one and the
+whole solve beside it; ``cpu_baseline`` (the oracle's reference-order restatement, one
+pinned core, bounded sample on the host of the GPU box); ``pcie_inclusive`` (host b and
+x: one H2D and one D2H per solve); ``one_pass_reorth`` (BASELINE configs[3]).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -33,21 +41,25 @@ sys.path.insert(0, os.path.join(ROOT, "two-pass-lanczos_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 METRIC = "Lanczos iterations/sec + SpMV GB/s (vs HBM roofline), 500k-arc KKT k=500"
+ARCS_SCALE = 5000000   # BASELINE configs[4]
+ORACLE_CFLAGS = "gcc 11 -O2 -mfma -ffp-contract=off -fno-fast-math (oracle/Makefile)"
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--k", type=int, default=500)
     p.add_argument("--arcs", type=int, default=0,
-                   help="5000/50000/500000 (netgen fixtures) or 5000000 (synthetic); "
+                   help="5000/50000/500000 (netgen fixtures) or any other count (synthetic); "
                         "default 500000 at N=1, 5000000 (row-partitioned) at N>1")
     p.add_argument("--partition", type=int, default=-1,
                    help="1: row-partitioned operator even at N=1 (default: N>1)")
     p.add_argument("--single-ref", type=int, default=1,
                    help="N>1: also time the same workload on rank 0's GPU alone")
+    p.add_argument("--scale-ref", type=int, default=1,
+                   help="N=1: also time BASELINE configs[4] (5M arcs) on this GPU")
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU leg")
     p.add_argument("--cpu-k", type=int, default=500, help="k of the bounded CPU sample")
     p.add_argument("--cpu-reps", type=int, default=2, help="CPU sample repetitions")
@@ -57,32 +69,39 @@ def parse():
     p.add_argument("--one-pass", type=int, default=1,
                    help="N=1: also time BASELINE configs[3] (one-pass k with CGS2 "
                         "re-orthogonalisation, V_k in HBM); 0 to skip")
-    return p.parse_args()
+    p.add_argument("--pcie", type=int, default=1, help="N=1: also time host b / x (PCIe)")
+    return p.parse_args(argv)
 
 
-def main():
-    args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo")  # barriers / max-reduce of host timings only
+def launch_command(argv, nproc: int, port: int) -> list:
+    """torch.distributed.run command line of the N-rank bench (one rank per GPU)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={nproc}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.join(ROOT, "bench.py")] + list(argv)
 
-    import numpy as np
-    import torch
 
-    import tpl_amd
-    from tpl_amd import _lib
-    from tpl_amd.error import check
-    from tpl_amd.utils.data_loader import load_kkt_system, write_qfc_3line
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    device = int(os.environ.get("TPL_DEVICE", local_rank))  # tests: ranks sharing one GPU
-    torch.cuda.set_device(device)
-    partitioned = (world > 1) if args.partition < 0 else bool(args.partition)
-    arcs = args.arcs or (5000000 if partitioned else 500000)
+
+def host_info() -> dict:
+    model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"nproc": os.cpu_count(), "allowed_cpus": len(os.sched_getaffinity(0)),
+            "cpu_model": model}
+
+
+def load_workload(arcs: int):
+    from tpl_amd.utils.data_loader import generate_kkt, load_kkt_system, write_qfc_3line
     if arcs in (5000, 50000, 500000):
         dmx = os.path.join(ROOT, "tests", "golden", "kkt", f"netgen-{arcs}-3.dmx.xz")
         qfc = os.path.join("/tmp", f"tpl_bench_{arcs}_{os.getpid()}.qfc")
@@ -92,23 +111,65 @@ def main():
         data = (f"netgen {arcs}-arc rho=3 instance regenerated from the reference's netgen "
                 "(tests/golden/kkt), b = A(1/sqrt(n))1, qfc 3-line (D empty)")
     else:
-        from tpl_amd.utils.data_loader import generate_kkt
         kkt = generate_kkt(arcs, seed=42)
         data = (f"synthetic {arcs}-arc rho=3 KKT (tpl_generate_kkt seed 42, "
                 f"{kkt.num_nodes} nodes), b = A(1/sqrt(n))1, D empty")
+    return kkt, data
+
+
+def time_solves(solve, reps: int, sync) -> float:
+    """Seconds per solve over `reps` calls after one untimed call."""
+    solve()
+    sync()
+    t = time.perf_counter()
+    for _ in range(reps):
+        solve()
+    sync()
+    return (time.perf_counter() - t) / reps
+
+
+def main():
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # parent of the N ranks: no GPU call here, no exec — a child, then its status
+        sys.exit(subprocess.call(launch_command(sys.argv[1:], args.gpus, _free_port())))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")  # barriers / max-reduce of host timings only
+
+    import ctypes
+
+    import numpy as np
+    import torch
+
+    import tpl_amd
+    from tpl_amd import _lib
+    from tpl_amd.error import check
+
+    device = int(os.environ.get("TPL_DEVICE", local_rank))  # rehearsal: ranks sharing one GPU
+    torch.cuda.set_device(device)
+    partitioned = (world > 1) if args.partition < 0 else bool(args.partition)
+    arcs = args.arcs or (ARCS_SCALE if partitioned else 500000)
+    kkt, data = load_workload(arcs)
     a = kkt.a
     n = a.shape[0]
     b = a @ np.full(n, 1.0 / np.sqrt(n))  # src/bin/tradeoff.rs:235-236
 
+    dctx = None
     if not partitioned:
         op = tpl_amd.HipCsrOp(a, device=device)
         b_loc = b
     else:
-        # row-partitioned operator: RCCL all-gather of the vector per SpMV over xGMI
+        # row-partitioned operator: RCCL exchanges over xGMI (DESIGN.md §7)
         if dist is None:
             import torch.distributed as dist
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", "29533")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
             dist.init_process_group("gloo", rank=0, world_size=1)
         from tpl_amd.dist import DistContext, DistHipCsrOp
         dctx = DistContext(rank, world, device=device,
@@ -148,12 +209,15 @@ def main():
         dt = float(t.item())
 
     # ---- roofline of the dominant kernel, measured live: HIP events recorded inside the
-    # last timed solve's captured pass two (on the operator's stream) bracket its
-    # steps_taken - 1 k_p2_spmv launches (launch gaps included).
+    # last timed solve's pass two (on the operator's stream) bracket its steps_taken - 1
+    # k_p2_spmv launches (launch gaps included). Bytes: SURVEY.md §8(d)'s B_spmv.
     p1_us, p2_us, p2_n = op.pass_timing()
     us = p2_us / p2_n
-    by = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
-    achieved = by / (us * 1e-6) / 1e9
+    b_spmv = op.algo_bytes(_lib.TPL_KERNEL_SPMV)
+    b_fused = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
+    achieved = b_spmv / (us * 1e-6) / 1e9
+    p1_step_us = p1_us / steps_taken
+    solve_s = dt / args.steps
     # isolated per-kernel event timings (graph of back-to-back launches), diagnostics only
     names = {_lib.TPL_KERNEL_PASS1_SPMV: "k_p1_spmv", _lib.TPL_KERNEL_PASS1_AXPY: "k_p1_axpy",
              _lib.TPL_KERNEL_PASS2_SPMV: "k_p2_spmv"}
@@ -161,13 +225,12 @@ def main():
     # HBM-side traffic of the same kernel from the committed PMC profile (rocprofv3 --pmc
     # FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 correction applied there)
     traffic, traffic_src = None, None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_k_p2_spmv.json")
+    pmc = os.path.join(ROOT, "profiles", "pmc_k_p2_spmv.json")
     if os.path.exists(pmc) and arcs == 500000 and not partitioned:
         with open(pmc) as f:
             pj = json.load(f)
         traffic, traffic_src = pj["traffic_bytes_per_launch"], pj["source"]
 
-    # N > 1: the ranks run ONE row-partitioned solve together (strong scaling)
     iters = args.steps * steps_taken
     value = iters / dt
     single = None
@@ -182,16 +245,9 @@ def main():
                 check(_lib.tpl_lanczos_two_pass(op1.handle, bd.data_ptr(), n, args.k,
                                                 _lib.FTK_INV_PTR, None, xd.data_ptr(),
                                                 _lib.TPL_MEM_DEVICE))
-            solve1()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                solve1()
-            torch.cuda.synchronize()
-            d1 = time.perf_counter() - t1
-            single = {"value": round(args.steps * steps_taken / d1, 2),
-                      "ms_per_step": round(1000.0 * d1 / args.steps, 4),
-                      "speedup_of_partition": round(d1 / dt, 3)}
+            d1 = time_solves(solve1, args.steps, torch.cuda.synchronize)
+            single = {"value": round(steps_taken / d1, 2), "ms_per_step": round(1000.0 * d1, 4),
+                      "speedup_of_partition": round(d1 / solve_s, 3)}
             op1.close()
         barrier()
     out = {
@@ -201,7 +257,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(1000.0 * dt / args.steps, 4),
+        "ms_per_step": round(1000.0 * solve_s, 4),
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,
@@ -218,24 +274,42 @@ def main():
                          + f", {dctx.transport})")},
         "roofline": {"bound": "hbm", "kernel": "k_p2_spmv" + ("" if not partitioned else
                                                              " (+ exchange, rank 0)"),
-                     "achieved": round(achieved, 1),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "algo_bytes_per_launch": by,
+                     "bytes_per_launch": b_spmv,
+                     "bytes_rule": "SURVEY.md §8(d) B_spmv = 12 nnz + 4 (n+1) + 16 n",
                      "avg_launch_us_events": round(us, 3),
-                     "pass1_us_per_step": round(p1_us / steps_taken, 3),
+                     "fused_bytes_per_launch": b_fused,
+                     "frac_fused_bytes": round(b_fused / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                     "pass1_us_per_step": round(p1_step_us, 3),
+                     "frac_pass1_step": round(b_spmv / (p1_step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                     "frac_whole_solve": round((2 * steps_taken - 1) * b_spmv / solve_s / 1e9
+                                               / HBM_PEAK_GBS, 4),
                      "kernels_us_isolated": iso},
     }
 
     if single is not None:
         out["single_gpu_same_workload"] = single
+    if args.pcie and not partitioned and world == 1:
+        # PCIe-inclusive rate (never `value`): host b in, host x out, one H2D + one D2H
+        xh = np.empty(n)
+        bh = np.ascontiguousarray(b)
+
+        def solve_h():
+            check(_lib.tpl_lanczos_two_pass(op.handle, bh.ctypes.data, n, args.k,
+                                            _lib.FTK_INV_PTR, None, xh.ctypes.data,
+                                            _lib.TPL_MEM_HOST))
+        th = time_solves(solve_h, max(args.steps, 3), torch.cuda.synchronize)
+        out["pcie_inclusive"] = {"iterations_per_s": round(steps_taken / th, 1),
+                                 "ms_per_solve": round(1000 * th, 4),
+                                 "note": "b and x in host memory (TPL_MEM_HOST)"}
     if args.one_pass and not partitioned:
         # BASELINE configs[3]: lanczos_standard (one pass, V_k in HBM) with CGS2 full
         # re-orthogonalisation, same instance and k; V stays on the device. The sweep
         # rate counts the algorithmic bytes of the re-orthogonalisation (per step j, two
         # passes of h = V_j^T r and r -= V_j h: 2 (16 n j + 24 n) bytes) over the time the
         # solve spends beyond the plain one-pass solve.
-        import ctypes
         PD = ctypes.POINTER(ctypes.c_double)
         al, be = np.zeros(args.k), np.zeros(args.k)
         st, bn = ctypes.c_size_t(0), ctypes.c_double(0.0)
@@ -245,15 +319,7 @@ def main():
                                             al.ctypes.data_as(PD), be.ctypes.data_as(PD),
                                             ctypes.byref(st), ctypes.byref(bn), None,
                                             _lib.TPL_MEM_DEVICE, reorth, None, None))
-            torch.cuda.synchronize()
-
-        tm = {}
-        for reorth in (0, 1):
-            one_pass(reorth)
-            t1 = time.perf_counter()
-            for _ in range(2):
-                one_pass(reorth)
-            tm[reorth] = (time.perf_counter() - t1) / 2
+        tm = {r: time_solves(lambda: one_pass(r), 2, torch.cuda.synchronize) for r in (0, 1)}
         s1 = int(st.value)
         rb = sum(2.0 * (16.0 * n * j + 24.0 * n) for j in range(1, s1))
         rate = rb / max(tm[1] - tm[0], 1e-9) / 1e9
@@ -268,11 +334,7 @@ def main():
         others = {}
         for arcs_o, k_o, f_o, ptr in ((5000, 50, "inv", _lib.FTK_INV_PTR),
                                       (50000, 200, "exp", _lib.FTK_EXP_PTR)):
-            qf = os.path.join("/tmp", f"tpl_bench_{arcs_o}_{os.getpid()}.qfc")
-            write_qfc_3line(qf, arcs_o)
-            ko = load_kkt_system(os.path.join(ROOT, "tests", "golden", "kkt",
-                                              f"netgen-{arcs_o}-3.dmx.xz"), qf)
-            os.unlink(qf)
+            ko, _ = load_workload(arcs_o)
             ao = ko.a
             no = ao.shape[0]
             opo = tpl_amd.HipCsrOp(ao, device=device)
@@ -282,40 +344,66 @@ def main():
             def solve_o():
                 check(_lib.tpl_lanczos_two_pass(opo.handle, bo.data_ptr(), no, k_o, ptr, None,
                                                 xo.data_ptr(), _lib.TPL_MEM_DEVICE))
-            solve_o()
-            torch.cuda.synchronize()
-            t1 = time.perf_counter()
-            for _ in range(10):
-                solve_o()
-            torch.cuda.synchronize()
-            dto = (time.perf_counter() - t1) / 10
+            dto = time_solves(solve_o, 10, torch.cuda.synchronize)
             others[f"{arcs_o}-arc k={k_o} f={f_o}"] = {
                 "ms_per_solve": round(1000 * dto, 3), "iterations_per_s": round(k_o / dto, 1),
                 "n": no, "nnz": int(ao.nnz)}
             opo.close()
         out["other_configs"] = others
+    if world == 1 and not partitioned and args.scale_ref:
+        # BASELINE configs[4]'s workload on this one GPU: the N = 1 point of the 1 -> N curve
+        # that the N > 1 lines measure (their `value` is this same solve, partitioned)
+        k5, _ = load_workload(ARCS_SCALE)
+        a5 = k5.a
+        n5 = a5.shape[0]
+        op5 = tpl_amd.HipCsrOp(a5, device=device)
+        b5 = torch.from_numpy(a5 @ np.full(n5, 1.0 / np.sqrt(n5))).cuda(device)
+        x5 = torch.empty_like(b5)
+
+        def solve5():
+            check(_lib.tpl_lanczos_two_pass(op5.handle, b5.data_ptr(), n5, args.k,
+                                            _lib.FTK_INV_PTR, None, x5.data_ptr(),
+                                            _lib.TPL_MEM_DEVICE))
+        op5.enable_timing(True)
+        d5 = time_solves(solve5, 3, torch.cuda.synchronize)
+        q1, q2, qn = op5.pass_timing()
+        u5 = q2 / qn
+        out["configs4_5m_1gpu"] = {
+            "workload": f"lanczos_two_pass k={args.k} f=inv, {ARCS_SCALE}-arc synthetic KKT "
+                        f"(n={n5}, nnz={a5.nnz}), one GPU",
+            "iterations_per_s": round(args.k / d5, 1), "ms_per_solve": round(1000 * d5, 3),
+            "k_p2_spmv_us": round(u5, 3),
+            "frac": round(op5.algo_bytes(_lib.TPL_KERNEL_SPMV) / (u5 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
+        op5.close()
     if rank == 0 and args.cpu_baseline and world == 1 and not partitioned:
         import oracle  # CPU baseline only (reference-order restatement, single thread)
         from oracle import ftk_ref
         o = oracle.Operator(a)
         kc = min(args.cpu_k, args.k)
         reps = max(1, args.cpu_reps)
-        t1 = time.perf_counter()
-        for _ in range(reps):
-            o.lanczos_two_pass(b, kc, ftk_ref.inv)
-        tc = (time.perf_counter() - t1) / reps
+        mask = os.sched_getaffinity(0)
+        core = min(mask)
+        os.sched_setaffinity(0, {core})  # one pinned core, as the reference's Par::Seq
+        oracle.set_threads(1)
+        try:
+            t1 = time.perf_counter()
+            for _ in range(reps):
+                o.lanczos_two_pass(b, kc, ftk_ref.inv)
+            tc = (time.perf_counter() - t1) / reps
+        finally:
+            os.sched_setaffinity(0, mask)
         out["cpu_baseline"] = {
             "value": round(kc / tc, 2), "unit": "Lanczos iterations/s", "cores": 1,
             "kind": "port",
-            "sample": f"oracle C restatement (reference order, gcc -O2, 1 thread) "
+            "sample": f"oracle C restatement (reference order, 1 thread pinned to cpu {core}) "
                       f"lanczos_two_pass k={kc} f=inv on the same instance, {reps} calls, "
                       f"{tc:.2f} s/call",
-        }
+            "compiler": ORACLE_CFLAGS, **host_info()}
         out["speedup_vs_cpu"] = round(value / (kc / tc), 1)
     if rank == 0:
         print(json.dumps(out), flush=True)
     op.close()
-    if partitioned:
+    if dctx is not None:
         dctx.close()
     if dist is not None:
         dist.barrier()

@@ -35,6 +35,6 @@ d = {"kernel": "k_p2_spmv", "config": "500k-arc KKT, lanczos_two_pass k=500 (ben
      "traffic_bytes_per_launch": round(2 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024),
      "correction": "2 x FETCH_SIZE (gfx950 half-count of wide reads) + WRITE_SIZE",
      "source": f"profiles/{tag}_pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE)"}
-with open(os.path.join(prof, "r01_pmc_k_p2_spmv.json"), "w") as f:
+with open(os.path.join(prof, "pmc_k_p2_spmv.json"), "w") as f:
     json.dump(d, f, indent=1)
 print(d)
