@@ -24,9 +24,9 @@
 //     is summed by 8 lanes (by a whole wave when longer than kBigPiece; those
 //     pieces lead the table). With S = 1 a piece is its whole row, finished in
 //     place. Otherwise every piece sum is published write-through into the row's
-//     slot (slots hold a sentinel while empty); after its store drains, the
-//     publisher reads the row's S slots, and the one that sees all S filled
-//     finalises the row (sums the slots, runs the epilogue, empties the slots).
+//     slot; after its store drains, the publisher adds 1 to the row's arrival counter
+//     (agent-scope atomic), and the one whose add returns the row's last count reads
+//     the S slots and finalises the row (sums the slots, runs the epilogue).
 //     Nobody waits on anybody.
 //
 // Canonical reduction order (reproduced bit for bit by oracle/lanczos_oracle.c):
@@ -97,9 +97,9 @@ constexpr int kPushMaxLong = 2048;   // pushed long rows: at most this many long
 constexpr int kPushSegLoads = (kPushMaxLong + kPushTPB) / kPushTPB;  // long rows per thread
 constexpr int kPushRun = 16;         // pushed runs longer than this are summed by a wave
 constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
-// Slice partial slots hold this signalling-NaN bit pattern while empty (arithmetic
-// never produces a signalling NaN, so a published partial can never equal it).
-constexpr unsigned long long kSliceSentinel = 0x7FF0DEAD0BADF00DULL;
+// Arrival counters of the sliced long rows: one uint32 per row, kCntStride apart (one
+// 64-B segment each, so the adds of different rows never share a segment).
+constexpr int kCntStride = 16;
 constexpr double kBreakdownTol = 2.220446049250313080847263336181640625e-13; // 1000*f64::EPSILON, src/algorithms/mod.rs:140-143
 
 // One bin-table slot: piece start (offset in the bin), long-row index, global row.
@@ -132,7 +132,8 @@ struct CsrDev {
   const void* b_val;        // double, or int8_t when val_i8
   const BinSeg* b_seg;      // n_bins x kTPB table slots (pieces, then the end marker)
   const int32_t* b_hdr;     // per bin: number of pieces | long pieces (first) << 16
-  double* P;                // n_long x kSlices piece partials (sentinel when empty)
+  double* P;                // n_long x kSlices piece partials (slot s: slice s)
+  unsigned int* Pcnt;       // n_long arrival counters, kCntStride apart (never reset)
   int32_t val_i8;           // 1: every stored value is a small integer, kept as int8
   int32_t s_col16;          // 1: chunk columns as uint16 offsets
   int32_t b_col16;          // 1: bin columns as uint16 offsets

@@ -614,28 +614,27 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
     epi.long_alpha(sg.ri, acc);
     return;
   }
-  // Hand-off, data-tagged: publish the piece sum write-through, drain, then read the
-  // row's S slots. The publisher whose store completed last sees all S, so
-  // some thread always finalises; a tie finalises twice, writing identical bits
-  // (every input — the slots, the row's vector entries loaded before publishing — is
-  // the same). No thread ever waits on another: nothing depends on dispatch order.
+  // Hand-off (MI355X_MICROARCH.md, valid forms, first table row): publish the piece sum
+  // write-through (sc1), drain this wave's stores, then ONE agent-scope atomic add on the
+  // row's arrival counter; the publisher whose add returns the row's last count (mod S:
+  // the counter runs on across launches, S divides 2^32) is the only one that reads the
+  // S slots (sc1 loads, after its add has returned) and finalises the row. The atomic
+  // adds of a row are totally ordered at the memory side, so exactly one publisher per
+  // launch sees the last count and every slot it reads was drained before the add that
+  // preceded its own. No thread ever waits on another: nothing depends on dispatch order.
   unsigned long long* slots = reinterpret_cast<unsigned long long*>(A.P + (size_t)sg.ri * kSlices);
   __hip_atomic_store(slots + s, (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   TPL_MARK(4);
+  const unsigned int arrived = __hip_atomic_fetch_add(A.Pcnt + (size_t)sg.ri * kCntStride, 1u,
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  asm volatile("" ::: "memory");  // the slot loads stay behind the returned add
+  if ((arrived & (unsigned)(ns - 1)) != (unsigned)(ns - 1)) return;
   unsigned long long v[kSlices];
 #pragma unroll
   for (int k = 0; k < kSlices; ++k)  // slots past the slice count: re-read slot 0
     v[k] = __hip_atomic_load(slots + (k < ns ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  bool all = true;
-#pragma unroll
-  for (int k = 0; k < kSlices; ++k) all = all && v[k] != kSliceSentinel;
-  if (!all) return;
-#pragma unroll
-  for (int k = 0; k < kSlices; ++k)  // empty again for the next launch
-    if (k < ns)
-      __hip_atomic_store(slots + k, kSliceSentinel, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   double y = 0.0;
 #pragma unroll
   for (int k = 0; k < kSlices; ++k)

@@ -556,6 +556,7 @@ struct tpl_op_s {
   void* d_bval = nullptr;
   BinSeg* d_bseg = nullptr;
   double* d_P = nullptr;
+  unsigned int* d_Pcnt = nullptr;
   int32_t* d_srows = nullptr;
   void* d_scol = nullptr;
   void* d_sval = nullptr;
@@ -620,6 +621,7 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.b_seg = op->d_bseg;
   A.b_hdr = op->d_bhdr;
   A.P = op->d_P;
+  A.Pcnt = op->d_Pcnt;
   A.s_width = L.s_width;
   A.s_identity = L.s_identity;
   A.n_short = (int32_t)L.srows.size();
@@ -709,10 +711,11 @@ void rebuild_schedule(tpl_op_s* op) {
     HIPCHK(hipMalloc(&op->d_tpP, cnt * sizeof(double)));
     HIPCHK(hipMemset(op->d_tpP, 0, cnt * sizeof(double)));
   }
-  // piece slots start empty (sentinel)
-  std::vector<unsigned long long> empty(std::max<size_t>(L.lrows.size() * kSlices, 1),
-                                        kSliceSentinel);
-  upload(reinterpret_cast<unsigned long long**>(&op->d_P), empty);
+  // piece slots, and the arrival counters of the sliced long rows (zero; they run on
+  // modulo the slice count across launches)
+  upload(&op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlices, 1), 0.0));
+  upload(&op->d_Pcnt,
+         std::vector<unsigned int>(std::max<size_t>(L.lrows.size() * kCntStride, 1), 0u));
   drop_graphs(op);
   // partial buffers depend on the layout: force state reallocation
   op->kcap = 0;
@@ -1229,6 +1232,7 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipStreamSynchronize(op->stream);
     drop_graphs(op);
     for (void* p : {(void*)op->d_bcol, (void*)op->d_bval, (void*)op->d_bseg, (void*)op->d_bhdr, (void*)op->d_P,
+                    (void*)op->d_Pcnt,
                     (void*)op->d_bcbase, (void*)op->d_scbase,
                     (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval,
                     (void*)op->d_cbase, (void*)op->d_cwidth, (void*)op->d_spos,
