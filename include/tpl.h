@@ -195,9 +195,9 @@ tpl_status tpl_generate_kkt(int64_t num_arcs, int64_t num_nodes, uint64_t seed,
 /* ---- introspection / measurement ---------------------------------------- */
 /* SpMV layout of the operator (DESIGN.md "SpMV layout"): rows with at most
  * short_row_max nnz ("short", ascending) are stored as sliced ELL, 512 rows per
- * chunk (512 x push_rpt with pushed long rows), one workgroup each; the n_long longer
- * rows (ascending) are either cut into S column slices (tpl_op_slices) handled by
- * XCD-local workgroups and summed by the last arriver, or pushed (tpl_op_push_layout).
+ * chunk, one workgroup each; the n_long longer rows (ascending) are cut into S column
+ * slices (tpl_op_slices) handled by XCD-local workgroups and summed by the last
+ * arriver.
  * G2 workgroups of E elements run the element-wise kernels (= #norm partials).
  * short_rows_out: n_short int32 or NULL; long_rows_out: n_long int32 or NULL.
  * The CPU oracle uses this to reproduce the device reduction order bit for bit.   */
@@ -209,20 +209,10 @@ tpl_status tpl_op_schedule(tpl_op_t op, int32_t* n_short, int32_t* n_long, int32
 tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g2);
 /* Column slices S of the long rows (1, 2, 4 or 8; part of the canonical reduction
  * order). tpl_op_set_slices rebuilds the layout with an explicit S
- * (0 = the auto rule: the fewest slices whose share of the vector fits a quarter of an L2,
+ * (0 = the auto rule: the fewest slices whose share of the vector fits an eighth of an L2,
  * more if a (row, slice) piece would not fit one bin).                          */
 tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices);
 tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices);
-/* Pushed long rows (single GPU): when every long-row entry (i, a) lies in
- * a short column and mirrors the short row's entry (a, i) bit for bit — the KKT
- * structure — the short-row chunks push the long rows' products and combiners finish
- * the long rows; no scattered gathers. *push = 1 when the layout uses it, *chunk_rows
- * = short-row positions per chunk (part of the canonical order). set_push: 0 = never
- * (default), 1 = whenever eligible; rebuilds the layout. Opt-in: pass one then needs
- * a third launch per step (the combiners run between the chunks and the alpha
- * reduction), which costs what pass two gains (measured trade-off).  */
-tpl_status tpl_op_push_layout(tpl_op_t op, int32_t* push, int32_t* chunk_rows);
-tpl_status tpl_op_set_push(tpl_op_t op, int32_t enable);
 
 /* Live timing of the solver's own launches: with timing on, HIP events on the
  * operator's stream bracket pass one's graph and the graph of pass two's step

@@ -58,8 +58,6 @@ typedef struct {
   int32_t G2;            /* element-wise workgroups == #norm partials */
   int64_t E;             /* elements per element-wise workgroup */
   int32_t slices;        /* column slices S of the long rows (1, 2, 4, 8) */
-  int32_t push;          /* 1: pushed long rows (tpl_push.hip) */
-  int32_t chunk_rows;    /* short-row positions per chunk (512, or 512 * push_rpt) */
 } osched;
 
 #define CHUNK 512        /* short-row positions per sliced-ELL chunk (kChunkRows) */
@@ -133,57 +131,6 @@ static double long_row_canon(const ocsr* A, int32_t i, const double* x, int S) {
   return y;
 }
 
-static int32_t chunk_rows(const osched* S) { return S->chunk_rows > 0 ? S->chunk_rows : CHUNK; }
-
-/* pushed long row (device: push_chunk + push_combine in tpl_push.hip): every entry
- * (i, c) lies in a short column c at short position p; the row's entries in chunk
- * w = p / C (positions ascending) form a run of L products round(a x): L <= PUSH_RUN:
- * P_w = 0; P_w += each in order; L > PUSH_RUN: lane l (0..63) sums the run's entries
- * l + 64q, tree64 (kPushRun in tpl_device.h); no entry: P_w = 0.
- * lane g (0..15): s_g = 0; s_g += P_w for w = g + 16q over ALL chunks (zeros
- * included); y = xor butterfly over the 16 lanes (1, 2, 4, 8).
- * pos: short position of every column (-1 for long rows). */
-#define PUSH_RUN 16
-static double push_run(const ocsr* A, const double* x, int64_t q0, int64_t q1) {
-  if (q1 - q0 <= PUSH_RUN) {
-    double s = 0.0;
-    for (int64_t q = q0; q < q1; ++q) s = s + A->v[q] * x[A->ci[q]];
-    return s;
-  }
-  double lane[64];
-  for (int l = 0; l < 64; ++l) {
-    double s = 0.0;
-    for (int64_t q = q0 + l; q < q1; q += 64) s = s + A->v[q] * x[A->ci[q]];
-    lane[l] = s;
-  }
-  return tree64(lane);
-}
-static double long_row_push(const ocsr* A, const osched* S, int32_t i, const double* x,
-                            const int32_t* pos, double* P) {
-  const int32_t C = chunk_rows(S);
-  const int32_t nch = (S->n_short + C - 1) / C;
-  for (int32_t w = 0; w < nch; ++w) P[w] = 0.0;
-  /* short positions ascend with the column (short rows ascending), so each chunk's
-   * entries are one contiguous stretch of the row */
-  for (int64_t q = A->rp[i]; q < A->rp[i + 1];) {
-    const int32_t w = pos[A->ci[q]] / C;
-    int64_t e = q;
-    while (e < A->rp[i + 1] && pos[A->ci[e]] / C == w) ++e;
-    P[w] = push_run(A, x, q, e);
-    q = e;
-  }
-  double lane[16], nx[16];
-  for (int g = 0; g < 16; ++g) {
-    lane[g] = 0.0;
-    for (int32_t w = g; w < nch; w += 16) lane[g] = lane[g] + P[w];
-  }
-  for (int h = 1; h < 16; h <<= 1) {
-    for (int g = 0; g < 16; ++g) nx[g] = lane[g] + lane[g ^ h];
-    memcpy(lane, nx, sizeof(nx));
-  }
-  return lane[0];
-}
-
 static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* y) {
   #pragma omp parallel for schedule(static)
   for (int32_t p = 0; p < S->n_short; ++p) {
@@ -191,16 +138,6 @@ static void spmv_canon(const ocsr* A, const osched* S, const double* x, double* 
     double s = 0.0;
     for (int64_t q = A->rp[i]; q < A->rp[i + 1]; ++q) s = s + A->v[q] * x[A->ci[q]];
     y[i] = s;
-  }
-  if (S->push && S->n_long > 0) {
-    int32_t* pos = (int32_t*)malloc(sizeof(int32_t) * (size_t)(ncols_of(A) + 1));
-    double* P = (double*)malloc(sizeof(double) * (size_t)(S->n_short / chunk_rows(S) + 2));
-    for (int64_t c = 0; c < ncols_of(A); ++c) pos[c] = -1;
-    for (int32_t p = 0; p < S->n_short; ++p) pos[S->srows[p]] = p;
-    for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_push(A, S, S->lrows[r], x, pos, P);
-    free(pos);
-    free(P);
-    return;
   }
   #pragma omp parallel for schedule(static)
   for (int32_t r = 0; r < S->n_long; ++r) y[S->lrows[r]] = long_row_canon(A, S->lrows[r], x, S->slices);
@@ -213,25 +150,21 @@ static void spmv(const ocsr* A, const osched* S, const double* x, double* y) {
 
 /* ------------------------------------------------------------ dot / norm */
 /* alpha = v . w in device order: short chunk c -> partial c (thread t owns short
- * positions C*c + t + NT q, C = chunk_rows, fma accumulation, tree over the NT threads:
- * NT = 256 -> tree256; pushed long rows: NT = 512 -> tree512 = ((S0+S1)+(S2+S3)) +
- * ((S4+S5)+(S6+S7)) of the 8 wave butterflies); long row r -> partial n_chunks + r =
- * round(v * w); then reduce_partials over all of them. */
+ * positions C*c + t + 256 q, C = CHUNK, fma accumulation, tree256); long row r ->
+ * partial n_chunks + r = round(v * w); then reduce_partials over all of them. */
 static double dot_canon(const osched* S, const double* v, const double* w, double* P) {
-  const int NT = S->push ? 2 * TPB : TPB;
-  const int32_t C = chunk_rows(S);
-  const int32_t nch = (S->n_short + C - 1) / C;
+  const int32_t nch = (S->n_short + CHUNK - 1) / CHUNK;
 #pragma omp parallel for schedule(static)
   for (int32_t c = 0; c < nch; ++c) {
-    double acc[2 * TPB];
-    for (int t = 0; t < NT; ++t) {
+    double acc[TPB];
+    for (int t = 0; t < TPB; ++t) {
       acc[t] = 0.0;
-      for (int q = 0; q < C / NT; ++q) {
-        const int32_t p = c * C + q * NT + t;
+      for (int q = 0; q < CHUNK / TPB; ++q) {
+        const int32_t p = c * CHUNK + q * TPB + t;
         if (p < S->n_short) acc[t] = fma(v[S->srows[p]], w[S->srows[p]], acc[t]);
       }
     }
-    P[c] = NT == TPB ? tree256(acc) : tree256(acc) + tree256(acc + TPB);
+    P[c] = tree256(acc);
   }
   for (int32_t r = 0; r < S->n_long; ++r) P[nch + r] = v[S->lrows[r]] * w[S->lrows[r]];
   return reduce_partials(P, nch + S->n_long);

@@ -22,9 +22,8 @@ n = a.shape[0]
 b = a @ np.full(n, 1 / np.sqrt(n))
 op = tpl_amd.HipCsrOp(a)
 op.set_slices(int(os.environ.get("SLICES", "0")))
-op.set_push(os.environ.get("PUSH", "0") == "1")
 tpl_amd.lanczos_two_pass(op, b, 50, "inv")
-row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "own": os.environ.get("TPL_OWNER_SLICES", ""), "slices": op.schedule()["slices"], "push": op.pushed}
+row = {"lib": os.path.basename(tpl_amd.LIB_PATH), "own": os.environ.get("TPL_OWNER_SLICES", ""), "slices": op.schedule()["slices"]}
 if os.environ.get("SOLVE", "1") == "1":  # full two-pass k=500 solves (ms, best of 5)
     import time
     tpl_amd.lanczos_two_pass(op, b, 500, "inv")

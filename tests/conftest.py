@@ -103,7 +103,7 @@ def short_row_threshold(lens, requested=-1):
     return max(4, min(32, 2 * m))
 
 
-def canon_schedule(a, short_row_max=-1, max_g2=1024, push=False):
+def canon_schedule(a, short_row_max=-1, max_g2=1024):
     """The device's layout rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp, build_layout)
     restated, for oracle runs without a GPU. The GPU tests take the layout from the
     live operator instead (HipCsrOp.schedule())."""
@@ -116,63 +116,17 @@ def canon_schedule(a, short_row_max=-1, max_g2=1024, push=False):
     g2 = max(1, min(max_g2, -(-n // ELEM_ROWS)))
     per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)
-    rpt = 0
-    if short.size and push:
-        # pushed long rows: short = the rows of the most common short length
-        hist = np.bincount(lens[short], minlength=T + 1)
-        hist[0] = 0
-        W = int(np.argmax(hist)) if hist.max() > 0 else 1
-        ps = np.nonzero(lens == W)[0].astype(np.int32) if short_row_max <= 0 else short
-        pl = np.nonzero(lens != W)[0].astype(np.int32) if short_row_max <= 0 else long_
-        rpt = push_rows_per_thread(a, ps, pl)
-        if rpt:
-            short, long_ = ps, pl
     return {"short_rows": short, "long_rows": long_, "G2": g2, "E": E,
-            "slices": auto_slices(a, long_), "push": int(rpt > 0),
-            "chunk_rows": 512 * rpt if rpt else 512}
-
-
-def push_rows_per_thread(a, short, long_, max_long=2048):
-    """tpl_runtime.cpp push_rows_per_thread: 1 or 4 when the long rows can be pushed
-    (every long-row entry in a short column, mirrored bit for bit by the short row;
-    uniform short width 1..4; chunks x long rows <= max(nnz_long / 2, 65536)), else 0."""
-    import scipy.sparse as sp
-    nl, ns = long_.size, short.size
-    if nl == 0 or nl > max_long or ns == 0:
-        return 0
-    lens = np.diff(a.indptr)
-    w = lens[short]
-    if w.min() != w.max() or not 1 <= w[0] <= 4:
-        return 0
-    is_long = np.zeros(a.shape[0], dtype=bool)
-    is_long[long_] = True
-    m = sp.csr_matrix(a)
-    L = m[long_]                       # long rows
-    if is_long[L.indices].any():
-        return 0                       # long-long entry
-    Ls = sp.csr_matrix(m[:, long_][short].T)  # short rows' long-column entries, transposed
-    Lsh = sp.csr_matrix(L[:, short])
-    if Ls.nnz != L.nnz or Lsh.nnz != L.nnz:
-        return 0
-    Ls.sort_indices()
-    Lsh.sort_indices()
-    if not (np.array_equal(Ls.indptr, Lsh.indptr) and np.array_equal(Ls.indices, Lsh.indices)
-            and np.array_equal(Ls.data.view(np.int64), Lsh.data.view(np.int64))):
-        return 0
-    budget = max(0.5 * L.nnz, 65536.0)
-    for rpt in (1, 4):
-        if -(-ns // (512 * rpt)) * nl <= budget:
-            return rpt
-    return 0
+            "slices": auto_slices(a, long_)}
 
 
 def auto_slices(a, long_rows, bin_max=7936):
     """tpl_runtime.cpp auto_slices + build_layout: the fewest of 1, 2, 4, 8 column slices
-    whose share of the vector (8 n bytes) fits 1 MiB, doubled while a (long row, slice)
+    whose share of the vector (8 n bytes) fits 512 KiB, doubled while a (long row, slice)
     piece holds more than bin_max entries."""
     n = a.shape[0]
     s = 1
-    while s < 8 and n * 8.0 / s > 1.0 * 1024 * 1024:
+    while s < 8 and n * 8.0 / s > 0.5 * 1024 * 1024:
         s *= 2
 
     def widest(S):

@@ -36,8 +36,7 @@ class _Rank:
 
     def __init__(self, a, rec, mode):
         sched = {"short_rows": rec["s_short"], "long_rows": rec["s_long"], "G2": int(rec["s_G2"]),
-                 "E": int(rec["s_E"]), "slices": int(rec["s_slices"]), "push": 0,
-                 "chunk_rows": 512}
+                 "E": int(rec["s_E"]), "slices": int(rec["s_slices"])}
         self.rows = np.asarray(rec["rows"], dtype=np.int64)
         self.n = self.rows.shape[0]
         if mode == "rows":

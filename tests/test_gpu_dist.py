@@ -43,12 +43,11 @@ def _run_ranks(tmp, world, transport, mode="auto", arcs=5000, k=50):
     return [np.load(os.path.join(tmp, f"rank{r}.npz")) for r in range(world)]
 
 
-def _single(kkt_tmp, arcs=5000, k=50, push=True):
+def _single(kkt_tmp, arcs=5000, k=50):
     import tpl_amd
     a = load_kkt(arcs, kkt_tmp).a
     b = harness_b(a)
     op = tpl_amd.HipCsrOp(a)
-    op.set_push(push)  # pushed long rows (partitioned operators always use bins)
     return (a, tpl_amd.lanczos_two_pass(op, b, k, "inv"),
             tpl_amd.algorithms.lanczos_pass_one(op, b, k), tpl_amd.lanczos(op, b, k, "inv"))
 
@@ -61,7 +60,7 @@ def _assemble(rs, key, n):
 
 
 def test_one_rank_rccl_rows_bitwise(kkt_tmp, tmp_path):
-    a, x, dec, xs = _single(kkt_tmp, push=False)  # same layout as the partition's
+    a, x, dec, xs = _single(kkt_tmp)  # same layout as the partition's
     r = _run_ranks(str(tmp_path), 1, "rccl", mode="rows")[0]
     assert str(r["mode"]) == "rows"
     assert np.array_equal(r["x1"], x)

@@ -76,30 +76,22 @@ def op5k(kkt5k):
 def test_schedule_matches_rule(which, skewed, kkt5k, kkt50k):
     a = {"skewed": skewed, "kkt5k": kkt5k.a, "kkt50k": kkt50k.a}[which]
     op = HipCsrOp(a)
-    for push in (False, True):
-        op.set_push(push)
-        sch = op.schedule()
-        ref = canon_schedule(a, push=push)
-        assert len(sch["short_rows"]) > 0 and len(sch["long_rows"]) > 0
-        assert np.array_equal(sch["short_rows"], ref["short_rows"])
-        assert np.array_equal(sch["long_rows"], ref["long_rows"])
-        assert sch["G2"] == ref["G2"] and sch["E"] == ref["E"]
-        assert sch["slices"] == ref["slices"]
-        # pushed long rows (opt-in) exactly for the KKT operators (mirrored entries)
-        assert sch["push"] == ref["push"] == (push and which != "skewed")
-        assert sch["chunk_rows"] == ref["chunk_rows"]
+    sch = op.schedule()
+    ref = canon_schedule(a)
+    assert len(sch["short_rows"]) > 0 and len(sch["long_rows"]) > 0
+    assert np.array_equal(sch["short_rows"], ref["short_rows"])
+    assert np.array_equal(sch["long_rows"], ref["long_rows"])
+    assert sch["G2"] == ref["G2"] and sch["E"] == ref["E"]
+    assert sch["slices"] == ref["slices"]
 
 
-@pytest.mark.parametrize("push", [True, False])
 @pytest.mark.parametrize("which", ["kkt5k", "kkt50k"])
-def test_push_and_bins_layouts_bitwise(push, which, kkt5k, kkt50k):
-    """Both long-row layouts of a KKT operator against the oracle in that layout's
-    order: SpMV, pass one, pass two with its basis (== pass one's, bit for bit), x."""
+def test_kkt_layouts_bitwise(which, kkt5k, kkt50k):
+    """The KKT operators against the oracle in the layout's order: SpMV, pass one, pass
+    two with its basis (== pass one's, bit for bit), x."""
     a = {"kkt5k": kkt5k.a, "kkt50k": kkt50k.a}[which]
     b = harness_b(a)
     op = HipCsrOp(a)
-    op.set_push(push)
-    assert op.pushed == push
     o = canon(op, a)
     x = std_rng_vector(a.shape[0]) - 0.5
     assert np.array_equal(op.apply(x), o.apply(x))

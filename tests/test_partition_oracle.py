@@ -49,7 +49,7 @@ def _replicated_records(a, cuts):
         g2 = max(1, min(1024, -(-n // 2048)))
         E = max(512, (-(-n // g2) + 511) // 512 * 512)
         s = 1
-        while s < 8 and n * 8.0 / s > 1024 * 1024:
+        while s < 8 and n * 8.0 / s > 512 * 1024:
             s *= 2
         recs.append({"rows": rows, "s_short": np.arange(ns, dtype=np.int32),
                      "s_long": np.arange(ns, n, dtype=np.int32), "s_G2": g2, "s_E": E,

@@ -13,7 +13,7 @@
 //     computed, not loaded, and the kernel is specialised for W.
 //   * LONG rows are cut into S column slices [floor(n*s/S), floor(n*(s+1)/S)), S in
 //     {1, 2, 4, 8} (tpl_runtime.cpp auto_slices: the fewest whose share of the
-//     gathered vector fits a quarter of an L2). The (row, slice) pieces of slice s, long
+//     gathered vector fits an eighth of an L2). The (row, slice) pieces of slice s, long
 //     rows ascending, are packed whole into BINS of bin_cap entries (padding
 //     col = -1) with at most kBinSegs pieces each; every slice gets the same number
 //     M of bins. Bin m of slice s is workgroup S*m + s of the slice part of the
@@ -40,19 +40,8 @@
 //                        8 lanes (offsets 1, 2, 4). L > kBigPiece: the same with 16
 //                        lanes (k = g + 16q) and a 16-lane butterfly (1, 2, 4, 8).
 //                        y = 0; y += P_s, s = 0..S-1.
-//   * long row, pushed : chunk w (positions [Cw, C(w+1)), C = 512 * push_rpt): the
-//                        row's entries in the chunk's short rows, ascending, are a run
-//                        of L products round(a_k x_k); L <= kPushRun: P_w = 0; P_w +=
-//                        each in order; L > kPushRun: lane g (0..63) sums the run's
-//                        entries g + 64q, then tree256's 64-lane butterfly -> P_w;
-//                        lane g (0..15): s_g = 0; s_g += P_w for
-//                        w = g + 16q (q ascending); y = xor butterfly of s over 16 lanes
-//                        (offsets 1, 2, 4, 8).
 //   * alpha partials   : Pa[c] (short chunk c): thread t: acc = fma(v, w, acc) over its
 //                        positions C*c + t + 256q (q ascending), tree256 (C = kChunkRows);
-//                        pushed long rows: C = 512 * push_rpt, positions C*c + t + 512q
-//                        (t < 512), tree512 = per-wave butterfly, then
-//                        ((S0 + S1) + (S2 + S3)) + ((S4 + S5) + (S6 + S7));
 //                        Pa[n_chunks + r] (long row r) = round(v * w).
 //                        alpha = partials(Pa[0 .. n_chunks + n_long)).
 //   * norm partial     : workgroup b (of G2) owns [bE, min(n,(b+1)E)); thread t visits
@@ -91,11 +80,6 @@ constexpr int kBinBatch = kBinMin / kTPB;  // entries per thread per load batch
 constexpr int kLongEpiRows = 1024;
 constexpr int kWinMax = 2048;        // short-chunk column window in LDS: at most this many columns
 constexpr int kWinLoads = kWinMax / 256;  // window loads per thread
-constexpr int kPushTPB = 512;        // threads per pushed-chunk / combiner workgroup (8 waves)
-constexpr int kCombRows = kPushTPB / 16;  // long rows per combiner workgroup (16 lanes each)
-constexpr int kPushMaxLong = 2048;   // pushed long rows: at most this many long rows
-constexpr int kPushSegLoads = (kPushMaxLong + kPushTPB) / kPushTPB;  // long rows per thread
-constexpr int kPushRun = 16;         // pushed runs longer than this are summed by a wave
 constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
 // Arrival counters of the sliced long rows: one uint32 per row, kCntStride apart (one
 // 64-B segment each, so the adds of different rows never share a segment).
@@ -158,20 +142,6 @@ struct CsrDev {
   int32_t long_defer;       // 1: long rows deferred to k_long_epi_*
   int32_t pad2;
   int64_t norm_n;           // == n except on ranks that do not own the replicated rows
-  // Pushed long rows (push == 1; single GPU; tpl_push.hip): no bins. Short rows sit in
-  // chunks of kPushTPB * push_rpt positions; each chunk pushes the products of its rows'
-  // long-column entries into LDS slots s_pos (sorted by long row, then position), sums
-  // every long row's run (tp_seg: n_long + 1 run starts per chunk) into one partial per
-  // (chunk, long row) — tpP[chunk * n_long + l] — and combiner workgroups (n_comb, 16
-  // long rows each) finish the long rows from those partials.
-  const uint16_t* s_pos;    // per sliced-ELL entry: LDS slot of its pushed product, 0xFFFF none
-  const uint16_t* tp_seg;   // n_chunks x (n_long + 1) run starts
-  const int32_t* lrows;     // n_long long rows (ascending)
-  double* tpP;              // 2 x n_chunks x n_long partials (ping-pong by step parity)
-  int32_t push;             // 1: pushed long rows
-  int32_t push_rpt;         // short rows per thread (chunk = kPushTPB * push_rpt positions)
-  int32_t n_comb;           // combiner workgroups = ceil(n_long / kCombRows)
-  int32_t tp_cap;           // LDS product slots (max pushed entries of one chunk)
   // Short-chunk column window (s_win > 0: every chunk's columns lie in [cbase, cbase +
   // s_win), s_win <= kWinMax; the window is staged in LDS). s_win_max: the largest
   // column of any chunk (window loads past it are clamped there).

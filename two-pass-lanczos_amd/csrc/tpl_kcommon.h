@@ -1,18 +1,9 @@
-// tpl_kcommon.h — device building blocks shared by the kernel translation units
-// (tpl_kernels.hip: element-wise, bins and pass kernels; tpl_push.hip: the pushed
-// long-row kernels): DPP reductions, epilogues, the sliced-ELL chunk and the
-// long-row bin. Included only by .hip files.
+// tpl_kcommon.h — device building blocks of the kernels (tpl_kernels.hip): DPP
+// reductions, epilogues, the sliced-ELL chunk and the long-row bin. Included only by
+// .hip files.
 #pragma once
 #include <hip/hip_runtime.h>
 #include "tpl_device.h"
-
-// Performance-ablation switches for experiments only (scripts/ablate.sh builds
-// separate libraries); production builds have TPL_ABLATE == 0. Bit 1: skip the
-// long-row bins; 2: skip the short chunks; 4: skip the bins' piece sums; 16 / 32: the
-// chunks' / bins' gathers read coalesced addresses instead (timing only).
-#ifndef TPL_ABLATE
-#define TPL_ABLATE 0
-#endif
 
 namespace tpl {
 
@@ -195,7 +186,7 @@ struct EpiPass1 {
   __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
   // long row r: its alpha partial is the single rounded product v * w
   __device__ __forceinline__ void long_alpha(int r, double acc) const { Pa_long[r] = acc; }
-  // returns v_j[i] (the value a pushed long row multiplies, tpl_push.hip)
+  // returns v_j[i]
   __device__ __forceinline__ double apply(int i, double s, const Pre1& p, double& acc) const {
     const double v = p.rc * invN_cur;
     const double vp = has_prev ? p.rp * invN_prev : 0.0;
@@ -232,7 +223,7 @@ struct EpiPass2 {
   __device__ __forceinline__ Pre2 pre(int i) const {
     return Pre2{v_cur[i], v_prev[i], nflush ? x[i] : 0.0};
   }
-  // returns v_{j+1}[i] (the value a pushed long row multiplies in the next step)
+  // returns v_{j+1}[i]
   __device__ __forceinline__ double apply(int i, double s, const Pre2& p, double&) const {
     const double vp = has_prev ? p.vp : 0.0;
     double w = s - beta_sub * vp;
@@ -265,9 +256,6 @@ __device__ __forceinline__ void p2_epi_ptrs(EpiPass2& epi, const double* v_cur, 
   epi.v_cur = v_cur;
   epi.v_prev = (j >= 2) ? v_prev : v_cur;
   epi.has_prev = j >= 2;
-#ifdef TPL_NO_X
-  nflush = 0;  // timing experiment only: no solution updates (wrong x)
-#endif
   epi.nflush = nflush;
   epi.v_next = v_next;
   epi.x = x;
@@ -373,7 +361,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
     for (int k = 0; k < W; ++k) {
       const int e = base + k * kChunkRows + q * kTPB + t;
       c[q][k] = col_at<C16>(A.s_col, e, cbase);
-      a[q][k] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.s_val, e);
+      a[q][k] = val_at<V8>(A.s_val, e);
     }
 #if !TPL_PRE_LATE
 #pragma unroll
@@ -392,7 +380,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 #pragma unroll
     for (int q = 0; q < kRowsPerThread; ++q)
 #pragma unroll
-      for (int k = 0; k < W; ++k) xv[q][k] = xsrc[(TPL_ABLATE & 16) ? (cbase + (t & 63)) : (c[q][k] < 0 ? 0 : c[q][k])];
+      for (int k = 0; k < W; ++k) xv[q][k] = xsrc[c[q][k] < 0 ? 0 : c[q][k]];
   }
 #if TPL_PRE_LATE
 #pragma unroll
@@ -500,9 +488,6 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                          const double* __restrict__ xsrc, ScaleFn scale_of,
                                          const Epi& epi, double* lds) {
   const int t = threadIdx.x;
-#ifdef TPL_BIN_PRIO
-  __builtin_amdgcn_s_setprio(TPL_BIN_PRIO);  // experiment: bins are the critical path
-#endif
   const int bin = __builtin_amdgcn_readfirstlane(m * A.n_slices + s);  // scalar loads below
   const int base = bin * A.bin_cap;
   const int cbase = C16 ? A.b_cbase[bin] : 0;
@@ -514,14 +499,14 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
 #pragma unroll
   for (int u = 0; u < kBinBatch; ++u) {
     c[u] = col_at<C16>(A.b_col, base + u * kTPB + t, cbase);
-    a[u] = (TPL_ABLATE & 8) ? 1.0 : val_at<V8>(A.b_val, base + u * kTPB + t);
+    a[u] = val_at<V8>(A.b_val, base + u * kTPB + t);
   }
   __builtin_amdgcn_sched_barrier(0);
   // only the slots up to the end marker are read (threads past it re-read the marker)
   const int npieces = hdr & 0xFFFF, nbig = hdr >> 16;
   const BinSeg sg = A.b_seg[bin * kTPB + (t < npieces ? t : npieces)];
 #pragma unroll
-  for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[(TPL_ABLATE & 32) ? ((base + u * kTPB + t) & 0x3FFFF) : (c[u] < 0 ? 0 : c[u])];
+  for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
   // the finalising thread's own row entries travel with the gathers
   auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
   const Scale sc = scale_of();
@@ -554,7 +539,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   // 16-lane group — lane g sums its entries g + 16q, then the 16-lane butterfly — 16
   // such pieces per pass (every piece of a bin at once at 500k arcs, where all pieces
   // are long); those pieces come first in the table (nbig of them).
-  if (!(TPL_ABLATE & 4)) {
+  {
     const int g16 = t & 15;
     for (int j0 = 0; j0 < nbig; j0 += kTPB / 16) {
       const int j = j0 + (t >> 4);
@@ -586,14 +571,12 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
     const int b0 = valid ? st : 0;
     const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
     double acc = 0.0;
-    if (!(TPL_ABLATE & 4)) {
-      for (int k0 = b0 + g8; k0 < en; k0 += 64) {  // 8 reads in flight, then the adds
-        double v[8];
+    for (int k0 = b0 + g8; k0 < en; k0 += 64) {  // 8 reads in flight, then the adds
+      double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
+      for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = k0 + 8 * u < en ? acc + v[u] : acc;
-      }
+      for (int u = 0; u < 8; ++u) acc = k0 + 8 * u < en ? acc + v[u] : acc;
     }
     acc = group8_sum(acc);
     if (g8 == 0 && valid) psum[j] = acc;
@@ -669,9 +652,6 @@ __device__ __forceinline__ int chunk_of_block(const CsrDev& A, int i) {
 #ifndef TPL_SPMV_MIN_WAVES
 #define TPL_SPMV_MIN_WAVES 1
 #endif
-#ifndef TPL_CHUNKS_FIRST
-#define TPL_CHUNKS_FIRST 0
-#endif
 // Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
 // index whose alpha partial this workgroup owns, or -1.
 // F = CW | V8 << 3 | SC16 << 4 | BC16 << 5 | WIN << 6: uniform chunk width (0: any), int8
@@ -680,15 +660,13 @@ template <int F, class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __restrict__ xsrc,
                                                ScaleFn scale_of, const Epi& epi, double& acc,
                                                double* lds) {
-  int b = blockIdx.x;
-  if (TPL_CHUNKS_FIRST) b = b < A.n_chunks ? b + A.n_slice_blocks : b - A.n_chunks;
+  const int b = blockIdx.x;
   if (b < A.n_slice_blocks) {
-    if (!(TPL_ABLATE & 1))
-      long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / A.n_slices, b % A.n_slices, xsrc, scale_of, epi, lds);
+    long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / A.n_slices, b % A.n_slices, xsrc, scale_of, epi, lds);
     return -1;
   }
   const int chunk = chunk_of_block(A, b - A.n_slice_blocks);
-  if (chunk < 0 || (TPL_ABLATE & 2)) return -1;  // grid padding
+  if (chunk < 0) return -1;  // grid padding
   return short_chunk<(F & 7), ((F >> 3) & 1), ((F >> 4) & 1), ((F >> 6) & 1)>(A, chunk, xsrc, scale_of, epi, acc, lds)
              ? chunk : -1;
 }

@@ -41,13 +41,6 @@ hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    int nflush, hipStream_t s);
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
                       hipStream_t s);
-// pushed long rows (tpl_push.hip)
-hipError_t push_p1(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
-                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
-hipError_t push_p2(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
-                   const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   int nflush, hipStream_t s);
-hipError_t push_spmv(const CsrDev& A, const double* x, double* y, int parity, hipStream_t s);
 hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
                        const double* r_cur, const double* r_prev, double* W, double* Vcol,
                        double* Pa_long, int j, hipStream_t s);
@@ -116,18 +109,17 @@ struct SchedParams {
   bool compress_values = true;      // int8 values when all values are small integers
   bool compress_cols = true;        // uint16 column offsets when the spans allow
   int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
-  int push = 0;                     // pushed long rows: -1 when eligible, 0 off (default)
 };
 
 // Column slices of the long rows (auto rule): the fewest (1, 2, 4, 8) whose share of
-// the gathered vector fits in a quarter of an XCD's 4 MiB L2 (measured at 500k arcs:
-// 4 slices 12.9 ms per k = 500 solve, 2 slices 13.5, 8 slices 15.4; at 50k: 1 slice
-// 7.1 ms, 2 slices 9.1) — slice s runs on the XCDs
+// the gathered vector fits in an eighth of an XCD's 4 MiB L2 (measured at 500k arcs with
+// the arrival-counter hand-off: 8 slices 11.91 ms per k = 500 solve, 4 slices 12.23, 2
+// slices 13.61; at 50k: 1 slice 7.1 ms, 2 slices 9.1) — slice s runs on the XCDs
 // b % 8 == s (mod slices), so each L2 caches only its slice's columns — and, when a
 // (row, slice) piece would exceed one bin, more slices until every piece fits.
 static int auto_slices(int64_t n_cols) {
   int s = 1;
-  while (s < kSlices && (double)n_cols * 8.0 / s > 1.0 * 1024.0 * 1024.0) s *= 2;
+  while (s < kSlices && (double)n_cols * 8.0 / s > 0.5 * 1024.0 * 1024.0) s *= 2;
   return s;
 }
 
@@ -154,58 +146,8 @@ struct Layout {
   int32_t M = 0;                    // bins per slice
   int G2 = 1;
   int64_t E = 512;
-  int32_t crows = kChunkRows;       // short-row positions per chunk
-  // pushed long rows (tpl_push.hip): no bins
-  bool push = false;
-  int32_t push_rpt = 0;
-  std::vector<uint16_t> s_pos;      // per sliced-ELL entry
-  std::vector<uint16_t> tp_seg;     // n_chunks x (n_long + 1)
-  int32_t tp_cap = 0;
   int32_t s_win = 0, s_win_max = 0;  // short-chunk column window (tpl_device.h)
 };
-
-// Rows per thread of the pushed layout, or 0 when the long rows cannot be pushed:
-// every long-row entry (i, a) must lie in a short column a and mirror the entry
-// (a, i) of short row a bit for bit (and no short row may hold an entry in a long
-// column that the long row lacks); the short rows need a uniform width of 1..4; and
-// the partials (chunks x long rows) must stay well below the long rows' nonzeros.
-static int32_t push_rows_per_thread(int64_t n, const std::vector<int32_t>& rp,
-                                    const std::vector<int32_t>& col,
-                                    const std::vector<double>& val,
-                                    const std::vector<int32_t>& srows,
-                                    const std::vector<int32_t>& lrows) {
-  const int64_t nl = (int64_t)lrows.size(), ns = (int64_t)srows.size();
-  if (nl == 0 || nl > kPushMaxLong || ns == 0) return 0;
-  std::vector<int32_t> lidx(n, -1);
-  for (int64_t l = 0; l < nl; ++l) lidx[lrows[l]] = (int32_t)l;
-  int32_t w = -1;
-  int64_t short_to_long = 0, long_nnz = 0;
-  for (int32_t r : srows) {
-    const int32_t len = rp[r + 1] - rp[r];
-    if (w < 0) w = len;
-    if (len != w) return 0;
-    for (int32_t q = rp[r]; q < rp[r + 1]; ++q) short_to_long += lidx[col[q]] >= 0;
-  }
-  if (w < 1 || w > 4) return 0;
-  for (int32_t i : lrows)
-    for (int32_t q = rp[i]; q < rp[i + 1]; ++q) {
-      const int32_t a = col[q];
-      if (lidx[a] >= 0) return 0;  // long-long entry
-      const auto b = col.begin() + rp[a], e = col.begin() + rp[a + 1];
-      const auto it = std::lower_bound(b, e, i);
-      if (it == e || *it != i) return 0;
-      const double mirror = val[it - col.begin()];
-      if (std::memcmp(&mirror, &val[q], sizeof(double)) != 0) return 0;
-      ++long_nnz;
-    }
-  if (long_nnz != short_to_long) return 0;
-  const double budget = std::max(0.5 * (double)long_nnz, 65536.0);
-  for (int32_t rpt : {1, 4}) {
-    const int64_t chunks = (ns + kPushTPB * rpt - 1) / (kPushTPB * rpt);
-    if ((double)chunks * (double)nl <= budget) return rpt;
-  }
-  return 0;
-}
 
 // Auto rule: T = clamp(2 * median row length, 4, kShortRowMax). A sliced-ELL chunk
 // costs as much as its widest row, so the few rows far above the typical length
@@ -247,39 +189,14 @@ struct ColMap {
 // single-GPU layout exactly).
 static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
                            const std::vector<int32_t>& col, const std::vector<double>& val,
-                           const SchedParams& sp, const ColMap& cmap, bool allow_push) {
+                           const SchedParams& sp, const ColMap& cmap) {
   Layout L;
   const int32_t T = short_row_threshold(n, rp, sp.short_row_max);
   for (int64_t i = 0; i < n; ++i) {
     if (sp.long_from >= 0 ? i >= sp.long_from : rp[i + 1] - rp[i] > T) L.lrows.push_back((int32_t)i);
     else L.srows.push_back((int32_t)i);
   }
-  if (allow_push && sp.push != 0) {
-    // Pushed long rows need short rows of ONE width: under the auto threshold, the
-    // short rows are the rows of the most common short length W (ties: the smaller),
-    // every other row is long (e.g. the few low-degree node rows of a KKT matrix).
-    std::vector<int32_t> sr = L.srows, lr = L.lrows;
-    if (sp.short_row_max <= 0 && sp.long_from < 0 && !L.srows.empty()) {
-      std::vector<int64_t> hist(T + 1, 0);
-      for (int32_t r : L.srows) hist[rp[r + 1] - rp[r]]++;
-      int32_t W = 1;
-      for (int32_t l = 1; l <= T; ++l)
-        if (hist[l] > hist[W]) W = l;
-      sr.clear();
-      lr.clear();
-      for (int64_t i = 0; i < n; ++i)
-        (rp[i + 1] - rp[i] == W ? sr : lr).push_back((int32_t)i);
-    }
-    L.push_rpt = push_rows_per_thread(n, rp, col, val, sr, lr);
-    L.push = L.push_rpt > 0;
-    if (L.push) {
-      L.crows = kPushTPB * L.push_rpt;
-      L.srows.swap(sr);
-      L.lrows.swap(lr);
-    }
-  }
   const int64_t ns = (int64_t)L.srows.size();
-  const int64_t kChunkRows = L.crows;  // (shadows the bins layout's constant)
   L.s_identity = 1;
   for (int64_t p = 0; p < ns; ++p)
     if (L.srows[p] != p) {
@@ -317,44 +234,10 @@ static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>
     if (uni && L.c_width[0] > 0) L.s_width = L.c_width[0];
   }
   const size_t nl = L.lrows.size();
-  if (L.push) {
-    // Pushed long rows: in chunk c, the entries of its short rows that lie in long
-    // columns get LDS slots sorted by (long row, position); tp_seg[c][l] = first slot
-    // of long row l (runs are contiguous, l ascending), tp_seg[c][nl] = the count.
-    std::vector<int32_t> lidx(n, -1);
-    for (size_t l = 0; l < nl; ++l) lidx[L.lrows[l]] = (int32_t)l;
-    L.s_pos.assign(L.s_col.size(), 0xFFFF);
-    L.tp_seg.assign((size_t)nchunks * (nl + 1), 0);
-    std::vector<std::pair<int64_t, int64_t>> items;  // (l * C + position-in-chunk, entry)
-    for (int64_t c = 0; c < nchunks; ++c) {
-      items.clear();
-      for (int64_t p = c * kChunkRows; p < std::min(ns, (c + 1) * kChunkRows); ++p) {
-        const int32_t r = L.srows[p];
-        for (int32_t k = 0; k < rp[r + 1] - rp[r]; ++k) {
-          const int32_t l = lidx[col[rp[r] + k]];
-          if (l < 0) continue;
-          const int64_t e = L.c_base[c] + (int64_t)k * kChunkRows + (p - c * kChunkRows);
-          items.emplace_back((int64_t)l * kChunkRows + (p - c * kChunkRows), e);
-        }
-      }
-      std::sort(items.begin(), items.end());
-      if (items.size() >= 0xFFFF) fail(TPL_ERR_UNSUPPORTED, "pushed chunk too wide");
-      uint16_t* seg = &L.tp_seg[(size_t)c * (nl + 1)];
-      size_t at = 0;
-      for (size_t l = 0; l <= nl; ++l) {
-        while (at < items.size() && items[at].first / kChunkRows < (int64_t)l) ++at;
-        seg[l] = (uint16_t)at;
-      }
-      for (size_t slot = 0; slot < items.size(); ++slot)
-        L.s_pos[items[slot].second] = (uint16_t)slot;
-      L.tp_cap = std::max<int32_t>(L.tp_cap, (int32_t)items.size());
-    }
-    L.tp_cap = std::max<int32_t>(L.tp_cap, 1);
-  }
   // Long rows: piece (r, s) = entries of long row r with columns in slice s (columns
   // [n_glob s / S, n_glob (s+1) / S)); the pieces of slice s, r ascending, are packed
-  // whole into bins (first fit in order). Pushed long rows have no bins.
-  const size_t nlb = L.push ? 0 : nl;
+  // whole into bins (first fit in order).
+  const size_t nlb = nl;
   int S = sp.slices > 0 ? sp.slices : auto_slices(n_glob);
   std::vector<int32_t> poff;
   int32_t widest = 0;
@@ -562,10 +445,6 @@ struct tpl_op_s {
   void* d_sval = nullptr;
   int32_t* d_cbase = nullptr;
   int32_t* d_cwidth = nullptr;
-  uint16_t* d_spos = nullptr;       // pushed long rows (tpl_push.hip)
-  uint16_t* d_tpseg = nullptr;
-  int32_t* d_lrows = nullptr;
-  double* d_tpP = nullptr;
   // vectors: b, R0..R2, W, x, V2_0..V2_2, tmp (n each, padded)
   double* d_vecs = nullptr;
   int64_t ld = 0;
@@ -638,14 +517,6 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * L.lrows.size() : nullptr;
   A.pad2 = 0;
   A.norm_n = op->hybrid && op->dist->rank != 0 ? op->ns_local : op->n;
-  A.s_pos = op->d_spos;
-  A.tp_seg = op->d_tpseg;
-  A.lrows = op->d_lrows;
-  A.tpP = op->d_tpP;
-  A.push = L.push ? 1 : 0;
-  A.push_rpt = L.push_rpt;
-  A.n_comb = (A.n_long + kCombRows - 1) / kCombRows;
-  A.tp_cap = L.tp_cap;
   A.s_win = L.s_win;
   A.s_win_max = L.s_win_max;
   A.n = op->n;
@@ -676,7 +547,7 @@ void rebuild_schedule(tpl_op_s* op) {
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, op->h_rowptr, op->h_col,
-                         op->h_val, op->sp, cmap, /*allow_push=*/op->dist == nullptr);
+                         op->h_val, op->sp, cmap);
   const Layout& L = op->lay;
   upload(&op->d_srows, L.srows);
   if (L.s_col16)
@@ -701,16 +572,6 @@ void rebuild_schedule(tpl_op_s* op) {
     upload(reinterpret_cast<double**>(&op->d_bval), L.b_val);
   upload(&op->d_bseg, L.b_seg);
   upload(&op->d_bhdr, L.b_hdr);
-  upload(&op->d_spos, L.s_pos);
-  upload(&op->d_tpseg, L.tp_seg);
-  upload(&op->d_lrows, L.lrows);
-  if (op->d_tpP) HIPCHK(hipFree(op->d_tpP));
-  op->d_tpP = nullptr;
-  if (L.push) {  // two partial buffers (step parity), chunks x long rows each
-    const size_t cnt = 2 * L.c_base.size() * L.lrows.size();
-    HIPCHK(hipMalloc(&op->d_tpP, cnt * sizeof(double)));
-    HIPCHK(hipMemset(op->d_tpP, 0, cnt * sizeof(double)));
-  }
   // piece slots, and the arrival counters of the sliced long rows (zero; they run on
   // modulo the slice count across launches)
   upload(&op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlices, 1), 0.0));
@@ -867,12 +728,6 @@ void enqueue_p1_prologue(tpl_op_s* op) {
 // Pass one, step j (k = requested steps).
 void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
   const CsrDev A = csr_dev(op);
-  if (A.push) {  // single GPU only (build_layout)
-    HIPCHK(launch::push_p1(A, op->S, r_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
-                           op->W, Vcol, j, op->stream));
-    HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
-    return;
-  }
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
                          op->W, Vcol, j, op->stream));
   if (op->hybrid) {
@@ -921,9 +776,6 @@ void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
 
 void enqueue_pass2_init(tpl_op_s* op, double* Vout) {
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, op->stream));
-  const CsrDev A = csr_dev(op);
-  // pushed long rows: the partials of A v_1 for step 1's combiners (buffer 1 % 2)
-  if (A.push) HIPCHK(launch::push_spmv(A, op->V2[1], nullptr, 1, op->stream));
   if (op->dist && !op->hybrid) dist_allgather(op, op->V2G[1], (size_t)op->ld);
 }
 void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
@@ -931,12 +783,6 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
   for (int j = 1; j < (int)steps; ++j) {
     double* Vcol = Vout ? Vout + (size_t)j * op->n : nullptr;
     const int nflush = p2_flush(j, (int)steps - 1);
-    if (A.push) {
-      HIPCHK(launch::push_p2(A, op->S, op->V2G[j % 3], op->V2[j % 3],
-                             j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
-                             Vcol, j, nflush, op->stream));
-      continue;
-    }
     HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
                            Vcol, j, nflush, op->stream));
@@ -1235,8 +1081,7 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
                     (void*)op->d_Pcnt,
                     (void*)op->d_bcbase, (void*)op->d_scbase,
                     (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval,
-                    (void*)op->d_cbase, (void*)op->d_cwidth, (void*)op->d_spos,
-                    (void*)op->d_tpseg, (void*)op->d_lrows, (void*)op->d_tpP})
+                    (void*)op->d_cbase, (void*)op->d_cwidth})
       if (p) hipFree(p);
     hipFree(op->d_vecs);
     if (op->d_rsum) hipFree(op->d_rsum);
@@ -1280,10 +1125,7 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
     upload_vec(op, op->tmp, x, mem);
     if (op->dist && !op->hybrid) dist_allgather(op, op->tmpG, (size_t)op->ld);
     const CsrDev A = csr_dev(op);
-    if (A.push)
-      HIPCHK(launch::push_spmv(A, op->tmpG, op->W, 0, op->stream));
-    else
-      HIPCHK(launch::spmv(A, op->tmpG, op->W, op->stream));
+    HIPCHK(launch::spmv(A, op->tmpG, op->W, op->stream));
     if (op->hybrid && A.n_long > 0) {
       dist_allgather(op, op->d_yall, (size_t)A.n_long);
       HIPCHK(launch::long_epi_y(A, op->d_yall, op->dist->nranks, op->W, op->stream));
@@ -1498,24 +1340,6 @@ tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices) {
   });
 }
 
-tpl_status tpl_op_push_layout(tpl_op_t op, int32_t* push, int32_t* chunk_rows) {
-  return guarded([&] {
-    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
-    if (push) *push = op->lay.push ? 1 : 0;
-    if (chunk_rows) *chunk_rows = op->lay.crows;
-  });
-}
-
-tpl_status tpl_op_set_push(tpl_op_t op, int32_t enable) {
-  return guarded([&] {
-    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
-    set_device(op);
-    op->sp.push = enable ? -1 : 0;
-    sync_checked(op);
-    rebuild_schedule(op);
-  });
-}
-
 tpl_status tpl_copy_to_host(void* dst, const void* src_device, size_t bytes) {
   return guarded([&] {
     if (bytes == 0) return;
@@ -1580,41 +1404,26 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     auto launch_one = [&](int i) {
       switch (kernel) {
         case TPL_KERNEL_SPMV:
-          if (A.push)
-            HIPCHK(launch::push_spmv(A, op->V2[0], op->W, 0, op->stream));
-          else
-            HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream));
+          HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream));
           break;
-        case TPL_KERNEL_PASS1_SPMV:  // pushed: both launches (chunks, then combiners)
-          if (A.push)
-            HIPCHK(launch::push_p1(A, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
-                                   op->stream));
-          else
-            HIPCHK(launch::p1_spmv(A, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
-                                   op->stream));
+        case TPL_KERNEL_PASS1_SPMV:
+          HIPCHK(launch::p1_spmv(A, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
+                                 op->stream));
           break;
         case TPL_KERNEL_PASS1_AXPY:
           HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
-          if (A.push)  // j = 2 + i keeps the partial buffers alternating as in a sweep
-            HIPCHK(launch::push_p2(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3],
-                                   op->V2[(i + 1) % 3], op->V2[i % 3], op->x, nullptr, 2 + (i & 1),
-                                   i % 3 == 2 ? 3 : 0, op->stream));
-          else
-            HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3], op->V2[(i + 1) % 3],
-                                   op->V2[i % 3], op->x, nullptr, 2, i % 3 == 2 ? 3 : 0,
-                                   op->stream));
+          HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3],
+                                 op->V2[(i + 1) % 3], op->V2[i % 3], op->x, nullptr, 2,
+                                 i % 3 == 2 ? 3 : 0, op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }
     };
     // Valid state for repeated launches: flags clear, partials/norms of a real step.
     HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
-    if (A.push)
-      HIPCHK(launch::push_p1(A, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
-    else
-      HIPCHK(launch::p1_spmv(A, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
+    HIPCHK(launch::p1_spmv(A, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
     HIPCHK(launch::p1_axpy(A, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[1], op->b, op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));

@@ -109,8 +109,6 @@ tpl_op_schedule = _sig("tpl_op_schedule", c_int, c_void_p, POINTER(c_int32), POI
 tpl_op_set_schedule = _sig("tpl_op_set_schedule", c_int, c_void_p, c_int32, c_int32)
 tpl_op_slices = _sig("tpl_op_slices", c_int, c_void_p, POINTER(c_int32))
 tpl_op_set_slices = _sig("tpl_op_set_slices", c_int, c_void_p, c_int32)
-tpl_op_push_layout = _sig("tpl_op_push_layout", c_int, c_void_p, POINTER(c_int32), POINTER(c_int32))
-tpl_op_set_push = _sig("tpl_op_set_push", c_int, c_void_p, c_int32)
 tpl_profile_kernel = _sig("tpl_profile_kernel", c_int, c_void_p, c_int, c_int, PD, PD)
 tpl_kernel_algo_bytes = _sig("tpl_kernel_algo_bytes", c_double, c_void_p, c_int)
 tpl_copy_to_host = _sig("tpl_copy_to_host", c_int, c_void_p, c_void_p, c_size_t)
@@ -135,7 +133,7 @@ EXPORTED = [
     "tpl_op_apply", "tpl_ftk_inv", "tpl_ftk_exp", "tpl_ftk_sq", "tpl_lanczos",
     "tpl_lanczos_two_pass", "tpl_lanczos_standard", "tpl_lanczos_pass_one",
     "tpl_lanczos_pass_two", "tpl_load_kkt_system", "tpl_csr_host_free", "tpl_op_schedule",
-    "tpl_op_set_schedule", "tpl_op_slices", "tpl_op_set_slices", "tpl_op_push_layout", "tpl_op_set_push", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
+    "tpl_op_set_schedule", "tpl_op_slices", "tpl_op_set_slices", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
     "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_generate_kkt", "tpl_op_flags",
     "tpl_op_set_value_format",
 ]

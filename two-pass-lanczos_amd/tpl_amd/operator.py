@@ -122,7 +122,7 @@ class HipCsrOp:
 
     # -- schedule / measurement ------------------------------------------------
     def schedule(self):
-        """Device layout: dict(short_rows, long_rows, G2, E, slices, push, chunk_rows) —
+        """Device layout: dict(short_rows, long_rows, G2, E, slices) —
         what the oracle needs to reproduce the device reduction order."""
         ns, nl, g2, e = c_int32(), c_int32(), c_int32(), c_int64()
         check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e), None, None))
@@ -133,11 +133,8 @@ class HipCsrOp:
                                    lr.ctypes.data_as(POINTER(c_int32))))
         sl = c_int32()
         check(_lib.tpl_op_slices(self._op, byref(sl)))
-        push, crows = c_int32(), c_int32()
-        check(_lib.tpl_op_push_layout(self._op, byref(push), byref(crows)))
         return {"short_rows": sr[:ns.value].copy(), "long_rows": lr[:nl.value].copy(),
-                "G2": g2.value, "E": e.value, "slices": sl.value, "push": push.value,
-                "chunk_rows": crows.value}
+                "G2": g2.value, "E": e.value, "slices": sl.value}
 
     def set_schedule(self, short_row_max=0, max_g2=0):
         check(_lib.tpl_op_set_schedule(self._op, short_row_max, max_g2))
@@ -145,14 +142,6 @@ class HipCsrOp:
     def set_slices(self, slices=0):
         """Column slices of the long rows: 1, 2, 4, 8, or 0 for the auto rule."""
         check(_lib.tpl_op_set_slices(self._op, slices))
-
-    def set_push(self, enable: bool = True):
-        """Pushed long rows when eligible, or never (the bins layout, the default)."""
-        check(_lib.tpl_op_set_push(self._op, 1 if enable else 0))
-
-    @property
-    def pushed(self) -> bool:
-        return bool(self.schedule()["push"])
 
     def profile_kernel(self, kernel: int, iters: int = 200):
         """(avg microseconds per launch, algorithmic bytes per launch) via HIP events."""
