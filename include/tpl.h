@@ -129,9 +129,16 @@ int tpl_ftk_sq(const double* alphas, size_t n_alphas, const double* betas, size_
 tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                        tpl_ftk_fn f, void* f_user, double* x_out, int mem);
 /* solvers::lanczos_two_pass (src/solvers.rs:133-175): pass one (scalars only),
- * f(T_k) on the host, y = y' ||b||, pass two regenerates V_k on the fly.        */
+ * f(T_k), y = y' ||b||, pass two regenerates V_k on the fly. With f == tpl_ftk_inv
+ * (single-GPU operator, k <= 1365, device f(T_k) on: tpl_op_set_device_ftk) the whole
+ * solve is ONE device graph — f(T_k) runs on the GPU with the host solver's exact
+ * operations (bitwise the same y), and no host round trip separates the passes. Any
+ * other f is called on the host between the passes. On an error x_out is unspecified. */
 tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                                 tpl_ftk_fn f, void* f_user, double* x_out, int mem);
+/* Device evaluation of the built-in inv in tpl_lanczos_two_pass: on != 0 (default)
+ * or off (the host solver between two graphs, as for a user f).                  */
+tpl_status tpl_op_set_device_ftk(tpl_op_t op, int on);
 
 /* ---- low-level API: src/algorithms/ -------------------------------------- */
 /* Per-step callback of lanczos_standard (LanczosCallback, src/algorithms/mod.rs:82-86):

@@ -7,7 +7,7 @@ OUT=$ROOT/gpurun_out
 mkdir -p "$OUT"
 cd "$ROOT"
 echo "== pytest -m gpu"
-timeout -k 10 ${TEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+timeout -k 10 ${TEST_TIMEOUT:-900} python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
 rc=$?
 tail -5 "$OUT/pytest_gpu.log"
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "pytest rc=$rc: stopping"; exit $rc; fi

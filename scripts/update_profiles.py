@@ -19,8 +19,10 @@ with open(os.path.join(out, "bench.log")) as f:
     line = [l for l in f if l.startswith("{")][-1]
 with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
     f.write(line)
-# the headline instance of k_p2_spmv: the variant with the largest traffic (smaller
-# configs of the same bench run instantiate other template variants)
+# the headline instance of k_p2_spmv: template variant 122 (500k KKT layout: uniform
+# width 2, int8 values, uint16 chunk and bin columns, chunk window); the other configs of
+# the same bench run (5k, 50k, 5M) instantiate other variants or share it with fewer calls
+HEADLINE = sys.argv[2] if len(sys.argv) > 2 else "k_p2_spmv<122>"
 blocks, cur = {}, None
 for l in open(os.path.join(out, "pmc_summary.txt")):
     if not l.startswith(" "):
@@ -29,7 +31,7 @@ for l in open(os.path.join(out, "pmc_summary.txt")):
     m = re.match(r"\s+(\S+)\s+([0-9.]+)", l)
     if m and cur and cur.startswith("k_p2_spmv"):
         blocks.setdefault(cur, {})[m.group(1)] = float(m.group(2))
-vals = max(blocks.values(), key=lambda v: v.get("FETCH_SIZE", 0.0))
+vals = blocks[HEADLINE]
 d = {"kernel": "k_p2_spmv", "config": "500k-arc KKT, lanczos_two_pass k=500 (bench.py --steps 1 --warmup 0)",
      "FETCH_SIZE_KiB": vals["FETCH_SIZE"], "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
      "traffic_bytes_per_launch": round(2 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024),

@@ -5,6 +5,7 @@ No compute on the GPU here."""
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -52,7 +53,7 @@ def test_version_and_no_device_is_reported_cleanly():
             tpl_amd.HipCsrOp(sp.identity(3).tocsr())
 
 
-@pytest.mark.parametrize("arcs", [5000, 50000])
+@pytest.mark.parametrize("arcs", [5000, 50000, 500000])
 def test_fixture_md5(arcs):
     assert md5_of_xz(os.path.join(KKT_DIR, f"netgen-{arcs}-3.dmx.xz")) == KKT_MD5[arcs]
 
@@ -147,18 +148,17 @@ def test_error_display_strings():
     assert LanczosError.parameter_mismatch("y_k", 1, 2) == LanczosError.parameter_mismatch("y_k", 1, 2)
 
 
-def test_netgen_fixture_regenerates_from_reference(tmp_path):
-    """tests/golden/make_fixtures.py recipe: the committed 5k fixture is byte-identical to
-    the reference's own netgen (compiled from /root/reference sources into oracle/_ref)."""
-    ng = os.path.join(ROOT, "oracle", "_ref", "netgen")
+@pytest.mark.parametrize("arcs", [5000, 50000, 500000])
+def test_netgen_fixture_regenerates_from_reference(arcs):
+    """tests/golden/make_fixtures.py: every committed netgen fixture (5k, 50k and the
+    500k headline instance) is byte-identical to the reference's own netgen (compiled
+    from /root/reference sources into oracle/_ref) run on the recorded parameters."""
     if not os.path.exists("/root/reference/data/netgen/src"):
         pytest.skip("reference checkout not present (GPU box)")
-    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle"), "ref"], check=True,
-                   capture_output=True)
-    out = subprocess.run([ng], input=b"1499034469\n1 115 6 7 5000 1 81 395 0 0 0 100 22 110\n",
-                         capture_output=True, check=True).stdout
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import make_fixtures
     import hashlib
-    assert hashlib.md5(out).hexdigest() == KKT_MD5[5000]
+    assert hashlib.md5(make_fixtures.generate(arcs)).hexdigest() == KKT_MD5[arcs]
 
 
 def test_harness_rng_matches_oracle_restatement():

@@ -1,0 +1,135 @@
+"""GPU: the one-graph two-pass solve — the built-in f = inv evaluated
+on the device (k_ftk_inv) between the passes, no host round trip.
+
+The device solver performs the host solver's operations in the same order
+(tpl_ftk.cpp tpl_ftk_inv, the dgtsv scheme), so the contract is BITWISE: the same x as
+the host-f path (two graphs around tpl_ftk_inv on the host) and as the canonical
+oracle, for every steps_taken residue mod 3 (the last step's pending x terms are added
+by k_p2_tail), under breakdown (the graph's step launches past steps_taken do
+nothing), with live timing on (three graphs) and for the error cases.
+Reference: src/solvers.rs:133-175, src/bin/tradeoff.rs:245-258.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+
+from conftest import harness_b
+
+pytestmark = pytest.mark.gpu
+
+import oracle  # noqa: E402
+from oracle.rng import std_rng_vector  # noqa: E402
+
+tpl_amd = pytest.importorskip("tpl_amd")
+from tpl_amd import HipCsrOp, LanczosError, LanczosErrorKind, ftk, solvers  # noqa: E402
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if tpl_amd.device_count() < 1:
+        pytest.skip("no GPU visible")
+
+
+def same_bits(x, y):
+    """Bitwise equality (NaN payloads included: T_1 = [0] is singular on the KKT runs)."""
+    return x.shape == y.shape and np.array_equal(x.view(np.int64), y.view(np.int64))
+
+
+def same_bits_nan(x, y):
+    """Bitwise where finite or infinite; NaN at the same places (host and device may
+    encode a NaN differently)."""
+    nx, ny = np.isnan(x), np.isnan(y)
+    return np.array_equal(nx, ny) and same_bits(x[~nx], y[~ny])
+
+
+def both_paths(op, b, k):
+    op.set_device_ftk(True)
+    xd = solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    op.set_device_ftk(False)
+    xh = solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    op.set_device_ftk(True)
+    return xd, xh
+
+
+@pytest.mark.parametrize("k", [1, 2, 3, 4, 49, 50, 51, 52])
+@pytest.mark.parametrize("rhs", ["harness", "rng"])
+def test_device_inv_bitwise_every_tail(k, rhs, kkt5k):
+    """steps_taken - 1 = 0..51 covers every pending-term count of the last step. With the
+    harness b (alpha == 0) an odd k gives a singular T_k: y' and x are non-finite on both
+    paths, and a NaN's encoding may differ between the host's and the device's
+    division, so NaN positions are compared, every other value bit for bit."""
+    a = kkt5k.a
+    op = HipCsrOp(a)
+    b = harness_b(a) if rhs == "harness" else std_rng_vector(a.shape[0])
+    xd, xh = both_paths(op, b, k)
+    assert same_bits_nan(xd, xh)
+    if rhs == "rng" or k % 2 == 0:
+        assert np.all(np.isfinite(xd)) and same_bits(xd, xh)
+    xo = oracle.Operator(a, op.schedule()).lanczos_two_pass(b, k, ftk.INV)
+    assert same_bits_nan(xd, xo)
+
+
+def test_device_inv_50k_k200_and_repeat(kkt50k):
+    a = kkt50k.a
+    op = HipCsrOp(a)
+    b = std_rng_vector(a.shape[0])
+    xd, xh = both_paths(op, b, 200)
+    assert same_bits(xd, xh)
+    assert same_bits(solvers.lanczos_two_pass(op, b, 200, ftk.INV), xd)  # graph replay
+
+
+def test_device_inv_breakdown_no_op_launches():
+    """Pass one stops at steps_taken < k (invariant subspace): the remaining step
+    launches of the one graph must leave x untouched."""
+    rng = np.random.default_rng(5)
+    n = 40
+    a = sp.diags(np.repeat(np.arange(1.0, 11.0), 4)).tocsr()  # 10 distinct eigenvalues
+    b = rng.standard_normal(n)
+    op = HipCsrOp(a)
+    for k in (12, 30):
+        xd, xh = both_paths(op, b, k)
+        assert same_bits(xd, xh)
+        dec = tpl_amd.algorithms.lanczos_pass_one(op, b, k)
+        assert dec.steps_taken <= 10
+    assert np.linalg.norm(a @ xd - b) / np.linalg.norm(b) < 1e-10
+
+
+def test_device_inv_timed_three_graphs(kkt5k):
+    a = kkt5k.a
+    op = HipCsrOp(a)
+    b = harness_b(a)
+    x0 = solvers.lanczos_two_pass(op, b, 50, ftk.INV)
+    op.enable_timing(True)
+    x1 = solvers.lanczos_two_pass(op, b, 50, ftk.INV)
+    p1_us, p2_us, n2 = op.pass_timing()
+    op.enable_timing(False)
+    assert same_bits(x0, x1)
+    assert n2 == 49 and p1_us > 0 and p2_us > 0
+
+
+def test_device_inv_zero_b_error(kkt5k):
+    op = HipCsrOp(kkt5k.a)
+    with pytest.raises(LanczosError) as e:
+        solvers.lanczos_two_pass(op, np.zeros(kkt5k.a.shape[0]), 10, ftk.INV)
+    assert e.value.kind == LanczosErrorKind.INPUT_ERROR
+    assert str(e.value) == "Invalid input parameter: Input vector `b` must not be a zero vector."
+    # the operator stays usable
+    b = harness_b(kkt5k.a)
+    xd, xh = both_paths(op, b, 10)
+    assert same_bits(xd, xh)
+
+
+def test_device_inv_device_pointers(kkt5k):
+    torch = pytest.importorskip("torch")
+    a = kkt5k.a
+    op = HipCsrOp(a)
+    b = harness_b(a)
+    x_host = solvers.lanczos_two_pass(op, b, 50, ftk.INV)
+    bd = torch.from_numpy(b).cuda()
+    xd = torch.empty_like(bd)
+    from tpl_amd import _lib
+    from tpl_amd.error import check
+    check(_lib.tpl_lanczos_two_pass(op.handle, bd.data_ptr(), a.shape[0], 50, _lib.FTK_INV_PTR,
+                                    None, xd.data_ptr(), _lib.TPL_MEM_DEVICE))
+    torch.cuda.synchronize()
+    assert same_bits(xd.cpu().numpy(), x_host)

@@ -631,21 +631,31 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   epi.long_alpha(sg.ri, acc);
 }
 
-// XCD-affine chunk order (speed only; any bijection is correct). Workgroups are dealt
-// round-robin to the 8 XCDs, block B on XCD B % 8 (observed on every launch: block 0
-// on XCD 0, scripts/lab/xcd_rr.hip), and an XCD's L2 keeps the lines a kernel wrote
-// there for the next kernel (scripts/lab/l2_keep.hip: 32 MB re-read 7.4 us on the
-// writing XCD vs 10.4 us elsewhere). Short chunk c (512 rows) lies in element-wise block
-// c / cpe (cpe = kElemRows / kChunkRows chunks per block), which k_p1_axpy / k_p1_init
-// run on XCD (c / cpe) % 8; the chunk part of an SpMV grid (padded to a multiple of
-// 8 cpe) places chunk c = 8 cpe q + cpe x + e on a block of XCD x, so the rows' vectors
-// (r, w, v, x) stay in one XCD's L2 from launch to launch. i: block index within the
-// chunk part; -1 for padding blocks.
+// XCD-contiguous placement (speed only; any bijection is correct). Workgroups are
+// dealt round-robin to the 8 XCDs, block B on XCD B % 8 (observed on every launch:
+// block 0 on XCD 0, scripts/lab/xcd_rr.hip), and an XCD's L2 keeps the lines a kernel
+// wrote there for the next kernel (scripts/lab/l2_keep.hip: 32 MB re-read 7.4 us on
+// the writing XCD vs 10.4 us elsewhere). Row block rb (A.E rows) therefore runs on XCD
+// x for rb in [rb_first(x), rb_first(x + 1)) — contiguous eighths of the rows — in every
+// kernel: the element-wise kernels (elem_block), the short chunks of the SpMV-shaped
+// kernels (chunk_of_block: chunk c lies in row block c / (E / kChunkRows)), and, with
+// 8 column slices, the bins of slice s (block 8m + s, on XCD s) gather exactly the
+// eighth of the vector that XCD s's chunks and element-wise blocks read and write.
+// Measured at 500k arcs (8 slices): k_p2_spmv 9.07 -> 8.55 us, solve 12.07 -> 11.70 ms
+// against 2048-row blocks dealt round-robin.
+__device__ __forceinline__ int rb_first(int G2, int x) { return (x * G2 + 7) >> 3; }
+// element-wise grid (8 ceil(G2 / 8) blocks): block i -> row block, or -1 (padding)
+__device__ __forceinline__ int elem_block(const CsrDev& A, int i) {
+  const int x = i & 7, q = i >> 3;
+  const int rb = rb_first(A.G2, x) + q;
+  return rb < rb_first(A.G2, x + 1) ? rb : -1;
+}
+// chunk part of an SpMV grid: block i of the part -> short chunk, or -1 (padding)
 __device__ __forceinline__ int chunk_of_block(const CsrDev& A, int i) {
-  constexpr int cpe = kElemRows / kChunkRows;  // chunks per element-wise block
-  const int x = ((i & 7) + A.n_slice_blocks) & 7;
-  const int c = (i / (8 * cpe)) * (8 * cpe) + cpe * x + ((i >> 3) % cpe);
-  return c < A.n_chunks ? c : -1;
+  const int cpe = (int)(A.E / kChunkRows);  // chunks per row block
+  const int x = (i + A.n_slice_blocks) & 7, q = i >> 3;
+  const int c = rb_first(A.G2, x) * cpe + q;
+  return (c < rb_first(A.G2, x + 1) * cpe && c < A.n_chunks) ? c : -1;
 }
 
 // Minimum waves per SIMD requested for the SpMV-shaped kernels (occupancy vs VGPRs).

@@ -49,7 +49,9 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
     S.flags[1] = 0;
     S.flags[2] = 0;
   }
-  const int64_t beg = (int64_t)blockIdx.x * A.E;
+  const int rb = elem_block(A, blockIdx.x);
+  if (rb < 0) return;
+  const int64_t beg = (int64_t)rb * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
   double acc = 0.0;
   for (int64_t i0 = beg + 2 * threadIdx.x; i0 < end; i0 += 2 * kTPB) {
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
     }
   }
   const double p = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pb[blockIdx.x] = p;
+  if (threadIdx.x == 0) S.Pb[rb] = p;
 }
 
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1), this rank's rows;
@@ -136,10 +138,12 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   asm volatile("" ::"s"(A.E), "s"(A.n), "s"(A.norm_n), "s"(A.NA_r), "s"(S.Pa_r), "s"(S.flags),
                "s"(S.norms), "s"(S.alphas), "s"(S.Pb));
   asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k));
+  const int rb = elem_block(A, blockIdx.x);
+  if (rb < 0) return;
   PartialRegs<12> pr;
   const int na_ = A.NA_r;
   load_partials(S.Pa_r, na_, pr);
-  const int64_t beg = (int64_t)blockIdx.x * A.E;
+  const int64_t beg = (int64_t)rb * A.E;
   const int64_t end = beg + A.E < A.n ? beg + A.E : A.n;
   // All of this thread's pairs (up to kAxPairs) are loaded before alpha is known, at
   // clamped addresses (vectors are padded to 64 doubles, so a pair starting below
@@ -166,7 +170,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   }
   if (stop) return;
   const double alpha = finish_partials(S.Pa_r, na_, pr, red);
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  if (rb == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
   }
@@ -199,15 +203,18 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     step(i0, *reinterpret_cast<const double2*>(W + i0),
          *reinterpret_cast<const double2*>(r_cur + i0));
   const double p = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pb[blockIdx.x] = p;
+  if (threadIdx.x == 0) S.Pb[rb] = p;
 }
 
 // Pass two prologue: v_1 = b * (1/||b||); x = v_1 * y_1 (src/algorithms/lanczos_two_pass.rs:248-252).
+// dyn: steps_taken is known only on the device (one-graph solve): nothing to do after
+// an error (zero b) or when pass one took no step.
 __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
                                                   const double* __restrict__ b,
                                                   double* __restrict__ v1,
                                                   double* __restrict__ x,
-                                                  double* __restrict__ Vcol) {
+                                                  double* __restrict__ Vcol, int dyn) {
+  if (dyn && (S.flags[1] || S.flags[2] < 1)) return;
   const double invN = 1.0 / S.norms[0];
   const double y0 = S.y[0];
   for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n;
@@ -228,23 +235,127 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, 
                                                   double* __restrict__ v_next,
                                                   double* __restrict__ x,
                                                   double* __restrict__ Vcol, int j,
-                                                  int nflush) {
+                                                  int nflush, int dyn) {
   extern __shared__ double lds[];
   pin_layout_args(A);
   asm volatile("" ::"s"(S.betas), "s"(S.alphas), "s"(S.y), "s"(xsrc), "s"(v_cur), "s"(v_prev),
-               "s"(v_next), "s"(x), "s"(Vcol), "s"(j), "s"(nflush));
+               "s"(v_next), "s"(x), "s"(Vcol), "s"(j), "s"(nflush), "s"(dyn), "s"(S.flags));
   EpiPass2 epi;
   p2_epi_ptrs(epi, v_cur, v_prev, v_next, x, Vcol, j, nflush);
   // The coefficients are read once the workgroup's entry and vector loads are in
   // flight (scale_of runs after them): a scalar load waited on at entry would put a
   // second dependent round trip in front of every workgroup.
+  // dyn (one-graph solve): the graph holds k - 1 step launches; those at or past
+  // steps_taken (pass one broke down early) do nothing.
   auto coefs = [&]() -> Scale {
     __builtin_amdgcn_sched_barrier(0);
+    if (dyn && j >= S.flags[2]) return Scale{0.0, false};
     p2_epi_coefs(epi, S, j, nflush);
     return Scale{1.0, true};
   };
   double acc = 0.0;
   spmv_block<F>(A, xsrc, coefs, epi, acc, lds);
+}
+
+// One-graph solve, after the k - 1 step launches: the x terms still pending at the last
+// step (last = steps_taken - 1 not a multiple of 3 — the step launches flush only at
+// multiples of 3, the host-side schedule p2_flush also at `last`), added exactly as the
+// last step's grouped flush would: x + y_{last-1} v_last (2 pending) + y_last v_{last+1}.
+__global__ __launch_bounds__(kTPB) void k_p2_tail(int64_t n, DevState S, double* __restrict__ x,
+                                                  const double* __restrict__ V0,
+                                                  const double* __restrict__ V1,
+                                                  const double* __restrict__ V2) {
+  if (S.flags[1]) return;
+  const int last = S.flags[2] - 1;
+  if (last < 1) return;
+  const int pending = last % 3;
+  if (pending == 0) return;
+  const double* ring[3] = {V0, V1, V2};
+  const double* vl = ring[last % 3];
+  const double* vn = ring[(last + 1) % 3];
+  const double y1 = S.y[last - 1], y0 = S.y[last];
+  for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kTPB) {
+    double xv = x[i];
+    if (pending == 2) xv = xv + y1 * vl[i];
+    x[i] = xv + y0 * vn[i];
+  }
+}
+
+// f(T_k) = T_k^{-1} on the device: y = ||b|| * T_k^{-1} e_1, the same operations in the
+// same order as the host solver tpl_ftk_inv (tpl_ftk.cpp: tridiagonal elimination with
+// partial pivoting, the LAPACK dgtsv scheme, then back substitution), so the two agree
+// bit for bit (IEEE division, -ffp-contract=off). The elimination is one dependent chain:
+// the 256 threads stage alpha and beta in LDS, lane 0 runs the chain with the running row
+// (d_i, du_i, b_i) in registers and the next row's inputs read ahead from LDS, the
+// eliminated rows go to LDS, and the back substitution writes y. One-graph solve only
+// (tpl_runtime.cpp): reads steps_taken and ||b|| from the solver state; dynamic LDS:
+// 6 kcap doubles.
+__global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
+  extern __shared__ double sh[];
+  const int n = S.flags[2];
+  if (S.flags[1] || n < 1) return;
+  double* al = sh;           // alpha (n)
+  double* be = sh + n;       // beta (n - 1)
+  double* D = sh + 2 * n;    // eliminated rows: d, du, du2, rhs
+  double* DU = sh + 3 * n;
+  double* DU2 = sh + 4 * n;
+  double* B = sh + 5 * n;
+  for (int i = threadIdx.x; i < n; i += kTPB) {
+    al[i] = S.alphas[i];
+    be[i] = i + 1 < n ? S.betas[i] : 0.0;
+  }
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const double bnorm = S.norms[0];
+  double di = al[0], dui = n > 1 ? be[0] : 0.0, bi = 1.0;
+  double nx_dl = n > 1 ? be[0] : 0.0, nx_d = n > 1 ? al[1] : 0.0, nx_du = n > 2 ? be[1] : 0.0;
+  for (int i = 0; i + 1 < n; ++i) {
+    const double dli = nx_dl, d1 = nx_d, du1 = nx_du;  // dl[i], d[i+1], du[i+1] (inputs)
+    if (i + 2 < n) {  // read ahead for row i + 1
+      nx_dl = be[i + 1];
+      nx_d = al[i + 2];
+      nx_du = i + 3 < n ? be[i + 2] : 0.0;
+    }
+    double dip1 = d1, duip1 = du1, bip1 = 0.0, du2i = 0.0;
+    if (fabs(di) >= fabs(dli)) {
+      const double fact = dli / di;
+      dip1 = dip1 - fact * dui;
+      bip1 = bip1 - fact * bi;
+      D[i] = di;
+      DU[i] = dui;
+      B[i] = bi;
+    } else {
+      const double fact = di / dli;
+      D[i] = dli;
+      const double temp = dip1;
+      dip1 = dui - fact * temp;
+      if (i + 2 < n) {
+        du2i = duip1;
+        duip1 = -fact * du2i;
+      }
+      DU[i] = temp;
+      B[i] = bip1;            // b[i] <- old b[i+1] (= 0: b[i+1] is first set at step i)
+      bip1 = bi - fact * bip1;
+    }
+    DU2[i] = du2i;
+    di = dip1;
+    dui = duip1;
+    bi = bip1;
+  }
+  // back substitution with U = (D, DU, DU2)
+  double x1 = bi / di;  // b[n-1] / d[n-1]
+  S.y[n - 1] = x1 * bnorm;
+  if (n > 1) {
+    double x0 = (B[n - 2] - DU[n - 2] * x1) / D[n - 2];
+    S.y[n - 2] = x0 * bnorm;
+    for (int ii = n - 3; ii >= 0; --ii) {
+      const double xi = (B[ii] - DU[ii] * x0 - DU2[ii] * x1) / D[ii];
+      S.y[ii] = xi * bnorm;
+      x1 = x0;
+      x0 = xi;
+    }
+  }
 }
 
 // ---------------------------------------- replicated long rows (partitioned solve)
@@ -450,11 +561,12 @@ static inline int elem_grid(int64_t n) {
   if (g < 1) g = 1;
   return (int)g;
 }
-// chunk part padded to a multiple of 8 x chunks per element block (chunk_of_block)
+// chunk part: 8 XCDs x the largest eighth of the row blocks x chunks per row block
 static inline int spmv_grid(const CsrDev& A) {
-  constexpr int g = 8 * (kElemRows / kChunkRows);
-  return A.n_slice_blocks + (A.n_chunks + g - 1) / g * g;
+  return A.n_slice_blocks + 8 * ((A.G2 + 7) / 8) * (int)(A.E / kChunkRows);
 }
+// element-wise kernels over the G2 row blocks (elem_block)
+static inline int g2_grid(const CsrDev& A) { return 8 * ((A.G2 + 7) / 8); }
 // dynamic LDS of the SpMV-shaped kernels: a bin's staged products + piece starts
 static inline size_t spmv_lds_bytes(const CsrDev& A) {
   const size_t bins = A.n_slice_blocks > 0
@@ -499,7 +611,7 @@ hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s) {
   return hipGetLastError();
 }
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_init, dim3(A.G2), dim3(kTPB), 0, s, A, S, b);
+  hipLaunchKernelGGL(k_p1_init, dim3(g2_grid(A)), dim3(kTPB), 0, s, A, S, b);
   return hipGetLastError();
 }
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
@@ -510,19 +622,28 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_axpy, dim3(A.G2), dim3(kTPB), 0, s, A, S, W, r_cur, r_next, j, k);
+  hipLaunchKernelGGL(k_p1_axpy, dim3(g2_grid(A)), dim3(kTPB), 0, s, A, S, W, r_cur, r_next, j, k);
   return hipGetLastError();
 }
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
-                   double* Vcol, hipStream_t s) {
-  hipLaunchKernelGGL(k_p2_init, dim3(elem_grid(n)), dim3(kTPB), 0, s, n, S, b, v1, x, Vcol);
+                   double* Vcol, int dyn, hipStream_t s) {
+  hipLaunchKernelGGL(k_p2_init, dim3(elem_grid(n)), dim3(kTPB), 0, s, n, S, b, v1, x, Vcol, dyn);
+  return hipGetLastError();
+}
+hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s) {
+  hipLaunchKernelGGL(k_p2_tail, dim3(elem_grid(n)), dim3(kTPB), 0, s, n, S, x, V[0], V[1], V[2]);
+  return hipGetLastError();
+}
+hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s) {
+  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)6 * kcap * sizeof(double), s, S);
   return hipGetLastError();
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   int nflush, hipStream_t s) {
+                   int nflush, int dyn, hipStream_t s) {
   if (spmv_grid(A) > 0)
-    return TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j, nflush);
+    return TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j, nflush,
+                         dyn);
   return hipGetLastError();
 }
 int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kLongEpiRows; }

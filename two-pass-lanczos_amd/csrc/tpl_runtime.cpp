@@ -33,12 +33,14 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s);
+hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
+hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
-                   double* Vcol, hipStream_t s);
+                   double* Vcol, int dyn, hipStream_t s);
 // nflush: x terms the step applies (tpl::p2_flush: every third step and the last)
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   int nflush, hipStream_t s);
+                   int nflush, int dyn, hipStream_t s);
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
                       hipStream_t s);
 hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
@@ -407,7 +409,14 @@ struct tpl_dist_s {
 };
 
 namespace {
-enum GraphKind { kGPass1 = 0, kGStandard = 1, kGPass2 = 2, kGPass2Steps = 3 };
+enum GraphKind {
+  kGPass1 = 0, kGStandard = 1, kGPass2 = 2, kGPass2Steps = 3,
+  kGTwoPassDev = 4,   // one-graph solve: pass one, device f(T_k), pass two
+  kGDevFtk = 5,       // (timed variant) device f(T_k) + pass-two prologue
+  kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
+};
+// One-graph solves keep the device f(T_k)'s working rows in LDS (6 k doubles, at most 64 KiB).
+constexpr size_t kDevFtkMaxK = 1365;
 }
 
 struct tpl_op_s {
@@ -467,6 +476,7 @@ struct tpl_op_s {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // live timing (tpl_op_enable_timing): events recorded inside the captured passes
   bool timing = false;
+  bool device_ftk = true;           // built-in inv evaluated on the device (one-graph solve)
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
 };
@@ -775,7 +785,7 @@ void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
 }
 
 void enqueue_pass2_init(tpl_op_s* op, double* Vout) {
-  HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, op->stream));
+  HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, 0, op->stream));
   if (op->dist && !op->hybrid) dist_allgather(op, op->V2G[1], (size_t)op->ld);
 }
 void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
@@ -785,7 +795,7 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
     const int nflush = p2_flush(j, (int)steps - 1);
     HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
-                           Vcol, j, nflush, op->stream));
+                           Vcol, j, nflush, 0, op->stream));
     if (op->hybrid) {
       const size_t nl = op->lay.lrows.size();
       if (nl) dist_allgather(op, op->d_yall, nl);
@@ -800,6 +810,26 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
 void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
   enqueue_pass2_init(op, Vout);
   enqueue_pass2_steps(op, steps, Vout);
+}
+
+// ---- one-graph two-pass solve (built-in f = inv, single GPU): steps_taken stays on the
+// device. Pass one as usual; k_ftk_inv forms y = ||b|| T^{-1} e_1 from the device alpha /
+// beta (bitwise the host solver's result); pass two is the k - 1 step launches, those at
+// or past steps_taken doing nothing, with x flushed at multiples of 3 only and the
+// pending terms of the last step added by k_p2_tail (the same sums as the host schedule).
+void enqueue_ftk_dev(tpl_op_s* op, size_t k) {
+  HIPCHK(launch::ftk_inv(op->S, (int)k, op->stream));
+  HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, nullptr, 1, op->stream));
+}
+void enqueue_pass2_dyn_steps(tpl_op_s* op, size_t k) {
+  const CsrDev A = csr_dev(op);
+  for (int j = 1; j < (int)k; ++j)
+    HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
+                           j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
+                           nullptr, j, j % 3 == 0 ? 3 : 0, 1, op->stream));
+}
+void enqueue_pass2_tail(tpl_op_s* op) {
+  HIPCHK(launch::p2_tail(op->n, op->S, op->x, op->V2, op->stream));
 }
 
 template <class Enq>
@@ -880,6 +910,29 @@ HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
   d.betas = d.alphas + kc;
   d.steps = (size_t)d.flags[2];
   return d;
+}
+
+// The whole two-pass solve as one graph (or, with live timing on, as three graphs with
+// the events between them); no host round trip between the passes.
+void run_two_pass_dev(tpl_op_s* op, size_t k) {
+  if (!op->timing) {
+    run_graph(op, kGTwoPassDev, k, [&] {
+      enqueue_pass1(op, k, false, false);
+      enqueue_ftk_dev(op, k);
+      enqueue_pass2_dyn_steps(op, k);
+      enqueue_pass2_tail(op);
+    });
+    return;
+  }
+  HIPCHK(hipEventRecord(op->tev[0], op->stream));
+  run_graph(op, kGPass1, k, [&] { enqueue_pass1(op, k, false, false); });
+  HIPCHK(hipEventRecord(op->tev[1], op->stream));
+  run_graph(op, kGDevFtk, k, [&] { enqueue_ftk_dev(op, k); });
+  HIPCHK(hipEventRecord(op->tev[2], op->stream));
+  run_graph(op, kGPass2Dyn, k, [&] { enqueue_pass2_dyn_steps(op, k); });
+  HIPCHK(hipEventRecord(op->tev[3], op->stream));
+  enqueue_pass2_tail(op);
+  op->p2_launches = (int64_t)k - 1;
 }
 
 void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV, bool reorth) {
@@ -1247,6 +1300,21 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
     set_device(op);
     check_b(op, b, b_len);
     check_k(k);
+    if (f == &tpl_ftk_inv && op->device_ftk && !op->dist && k <= kDevFtkMaxK) {
+      // one graph: pass one, y = ||b|| T^{-1} e_1 on the device, pass two (the built-in
+      // inv is the same computation as on the host, bit for bit; src/solvers.rs:148-174)
+      ensure_state(op, k);
+      upload_vec(op, op->b, b, mem);
+      run_two_pass_dev(op, k);
+      download_vec(op, x_out, op->x, op->n, mem);
+      HIPCHK(hipMemcpyAsync(op->h_state, op->d_state, 16, hipMemcpyDeviceToHost, op->stream));
+      sync_checked(op);
+      int32_t flags[4];
+      std::memcpy(flags, op->h_state, 16);
+      if (flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+      if (flags[2] == 0) zero_out(op, x_out, mem);
+      return;
+    }
     // 1. pass one (src/solvers.rs:148)
     run_pass_one(op, b, k, mem, false, false);
     const HostDecomp d = fetch_decomp(op, k);
@@ -1365,6 +1433,13 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
   }
 }
 
+tpl_status tpl_op_set_device_ftk(tpl_op_t op, int on) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    op->device_ftk = on != 0;
+  });
+}
+
 tpl_status tpl_op_enable_timing(tpl_op_t op, int on) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
@@ -1416,7 +1491,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
         case TPL_KERNEL_PASS2_SPMV:
           HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3],
                                  op->V2[(i + 1) % 3], op->V2[i % 3], op->x, nullptr, 2,
-                                 i % 3 == 2 ? 3 : 0, op->stream));
+                                 i % 3 == 2 ? 3 : 0, 0, op->stream));
           break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }

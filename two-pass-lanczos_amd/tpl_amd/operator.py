@@ -149,6 +149,11 @@ class HipCsrOp:
         check(_lib.tpl_profile_kernel(self._op, kernel, iters, byref(us), byref(by)))
         return us.value, by.value
 
+    def set_device_ftk(self, on: bool = True):
+        """Built-in inv of lanczos_two_pass evaluated on the device, the solve as one graph
+        (default), or on the host between the passes."""
+        check(_lib.tpl_op_set_device_ftk(self._op, 1 if on else 0))
+
     def enable_timing(self, on: bool = True):
         """Record HIP events inside the captured passes of later solves."""
         check(_lib.tpl_op_enable_timing(self._op, 1 if on else 0))
