@@ -83,7 +83,8 @@ int64_t tpl_op_nnz(tpl_op_t op);
 /* Bit 0: row-partitioned operator; bit 1: passes launched eagerly (no hipGraph —
  * a host transport, or a transport that refused stream capture); bit 2: values kept
  * as int8, bit 3 / bit 4: short-row / long-row column indices kept as uint16 offsets
- * (see tpl_op_set_value_format). -1 if op is NULL.                                 */
+ * (see tpl_op_set_value_format), bit 5: the last tpl_lanczos_two_pass ran as one
+ * device graph (device f(T_k)). -1 if op is NULL.                                  */
 int tpl_op_flags(tpl_op_t op);
 /* Storage format (rebuilds the layout): compress != 0 (default) keeps the values as
  * int8 when every one is an integer in [-128, 127] (not -0.0), and the column
@@ -129,16 +130,18 @@ int tpl_ftk_sq(const double* alphas, size_t n_alphas, const double* betas, size_
 tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                        tpl_ftk_fn f, void* f_user, double* x_out, int mem);
 /* solvers::lanczos_two_pass (src/solvers.rs:133-175): pass one (scalars only),
- * f(T_k), y = y' ||b||, pass two regenerates V_k on the fly. With f == tpl_ftk_inv
- * (single-GPU operator, k <= 1365, device f(T_k) on: tpl_op_set_device_ftk) the whole
- * solve is ONE device graph — f(T_k) runs on the GPU with the host solver's exact
- * operations (bitwise the same y), and no host round trip separates the passes. Any
- * other f is called on the host between the passes. On an error x_out is unspecified. */
+ * f(T_k), y = y' ||b||, pass two regenerates V_k on the fly. With f == tpl_ftk_inv on a
+ * single-GPU operator the solve can run as ONE device graph: f(T_k) on the GPU with the
+ * host solver's exact operations (bitwise the same y), no host round trip between the
+ * passes (tpl_op_set_device_ftk). Any other f is called on the host between the passes.
+ * On an error x_out is unspecified.                                               */
 tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                                 tpl_ftk_fn f, void* f_user, double* x_out, int mem);
-/* Device evaluation of the built-in inv in tpl_lanczos_two_pass: on != 0 (default)
- * or off (the host solver between two graphs, as for a user f).                  */
-tpl_status tpl_op_set_device_ftk(tpl_op_t op, int on);
+/* Where tpl_lanczos_two_pass evaluates the built-in inv: mode 0 = host (two graphs),
+ * 1 = device for k <= 1365 (one graph), 2 = auto (default): device for k <= 128, where
+ * the single-lane device solve (a chain of ~2k divisions) costs no more than the host
+ * round trip it removes.                                                          */
+tpl_status tpl_op_set_device_ftk(tpl_op_t op, int mode);
 
 /* ---- low-level API: src/algorithms/ -------------------------------------- */
 /* Per-step callback of lanczos_standard (LanczosCallback, src/algorithms/mod.rs:82-86):
@@ -146,7 +149,11 @@ tpl_status tpl_op_set_device_ftk(tpl_op_t op, int on);
  * V_k (column-major, ld = n, k valid columns) and the host T_k scalars
  * (k alphas, k-1 betas... exactly the reference's TridiagonalSystemView, i.e.
  * betas holds the betas pushed so far). Return non-zero to continue, 0 to stop.
- * Supplying a callback forces one host synchronisation per step (slow path).   */
+ * The host polls in batches (1, 2, 4, ... up to 32 steps run ahead on the device, then
+ * the callback for each of them in order): a stop at step j returns exactly the
+ * j-step result (later steps never change earlier coefficients or columns), with one
+ * host synchronisation per batch. Columns past k may already hold later basis
+ * vectors while the callback runs; only the first k are the view.               */
 typedef int (*tpl_step_cb)(size_t k, const double* v_k_device, int64_t n,
                            const double* alphas, size_t n_alphas, const double* betas,
                            size_t n_betas, void* user);
@@ -220,6 +227,14 @@ tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g
  * more if a (row, slice) piece would not fit one bin).                          */
 tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices);
 tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices);
+
+/* Device memory the operator holds now, in bytes: its layout (matrix in the engine's
+ * format), the ten n-vectors of the recurrence, the solver state and — once a one-pass
+ * solve (tpl_lanczos / tpl_lanczos_standard) has run — the basis V_k (8 n k bytes).
+ * This is the device-side counterpart of the reference's peak-memory column
+ * (src/utils/perf.rs:16-31, results/scalability_*.csv rss_kb): the two-pass variant
+ * never allocates V_k.                                                            */
+tpl_status tpl_op_device_bytes(tpl_op_t op, uint64_t* bytes);
 
 /* Live timing of the solver's own launches: with timing on, HIP events on the
  * operator's stream bracket pass one's graph and the graph of pass two's step

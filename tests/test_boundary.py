@@ -167,3 +167,18 @@ def test_harness_rng_matches_oracle_restatement():
     from oracle.rng import std_rng_vector
     assert np.array_equal(std_rng_f64(10000, 42), std_rng_vector(10000, 42))
     assert np.array_equal(std_rng_f64(7, 3), std_rng_vector(7, 3))
+
+
+def test_operator_input_is_copied_and_canonicalised():
+    """HipCsrOp's host conversion (no GPU needed) never touches the caller's matrix and
+    sums duplicates like faer's try_new_from_triplets; explicit zeros stay."""
+    from tpl_amd.operator import _as_csr_arrays
+    indptr = np.array([0, 3, 4, 5])
+    indices = np.array([2, 0, 2, 1, 0], dtype=np.int32)   # unsorted, (0, 2) twice
+    data = np.array([1.0, 5.0, 2.0, 0.0, 3.0])
+    m = sp.csr_matrix((data, indices, indptr), shape=(3, 3))
+    before = (m.indices.copy(), m.data.copy())
+    n, rp, ci, v = _as_csr_arrays(m)
+    assert np.array_equal(m.indices, before[0]) and np.array_equal(m.data, before[1])
+    assert n == 3 and list(rp) == [0, 2, 3, 4]
+    assert list(ci) == [0, 2, 1, 0] and list(v) == [5.0, 3.0, 0.0, 3.0]

@@ -42,12 +42,17 @@ def same_bits_nan(x, y):
     return np.array_equal(nx, ny) and same_bits(x[~nx], y[~ny])
 
 
+ONE_GRAPH = 32  # tpl_op_flags bit 5: the last two-pass solve ran as one device graph
+
+
 def both_paths(op, b, k):
     op.set_device_ftk(True)
     xd = solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    assert op.flags() & ONE_GRAPH, "the one-graph path was not taken"
     op.set_device_ftk(False)
     xh = solvers.lanczos_two_pass(op, b, k, ftk.INV)
-    op.set_device_ftk(True)
+    assert not op.flags() & ONE_GRAPH
+    op.set_device_ftk(2)
     return xd, xh
 
 
@@ -94,10 +99,26 @@ def test_device_inv_breakdown_no_op_launches():
     assert np.linalg.norm(a @ xd - b) / np.linalg.norm(b) < 1e-10
 
 
+def test_auto_mode(kkt5k):
+    """Default (auto): one graph for k <= 128, the host solver between two graphs above."""
+    a = kkt5k.a
+    op = HipCsrOp(a)
+    b = std_rng_vector(a.shape[0])
+    solvers.lanczos_two_pass(op, b, 128, ftk.INV)
+    assert op.flags() & ONE_GRAPH
+    solvers.lanczos_two_pass(op, b, 129, ftk.INV)
+    assert not op.flags() & ONE_GRAPH
+    solvers.lanczos_two_pass(op, b, 50, ftk.EXP)  # a host f is never moved to the device
+    assert not op.flags() & ONE_GRAPH
+    with pytest.raises(tpl_amd.TplError):
+        op.set_device_ftk(3)
+
+
 def test_device_inv_timed_three_graphs(kkt5k):
     a = kkt5k.a
     op = HipCsrOp(a)
     b = harness_b(a)
+    op.set_device_ftk(1)
     x0 = solvers.lanczos_two_pass(op, b, 50, ftk.INV)
     op.enable_timing(True)
     x1 = solvers.lanczos_two_pass(op, b, 50, ftk.INV)
@@ -124,6 +145,7 @@ def test_device_inv_device_pointers(kkt5k):
     a = kkt5k.a
     op = HipCsrOp(a)
     b = harness_b(a)
+    op.set_device_ftk(1)
     x_host = solvers.lanczos_two_pass(op, b, 50, ftk.INV)
     bd = torch.from_numpy(b).cuda()
     xd = torch.empty_like(bd)

@@ -45,14 +45,40 @@ def test_orthogonality_rows_match_published():
         assert r["ortho_loss_regenerated"] == r["ortho_loss_standard"]
 
 
-def test_tradeoff_schema(tmp_path):
+def test_tradeoff_schema_and_memory_tradeoff(tmp_path):
+    """src/bin/tradeoff.rs: one fresh worker per variant, rows grouped by variant (the
+    orchestrator appends each worker's output), k ascending; the device column shows the
+    reference's trade-off — the standard variant holds V_k (8 n k bytes), the two-pass
+    variant's footprint does not grow with k."""
     from tpl_amd import harness
     out = str(tmp_path / "t.csv")
-    harness.main(["tradeoff", "--arcs", "5000", "--k-start", "50", "--k-end", "100",
+    harness.main(["tradeoff", "--arcs", "5000", "--k-start", "50", "--k-end", "150",
                   "--k-step", "50", "--output", out])
     with open(out) as f:
         rows = list(csv.DictReader(f))
-    assert list(rows[0].keys()) == ["variant", "k", "time_s", "rss_kb"]
+    assert list(rows[0].keys()) == ["variant", "k", "time_s", "rss_kb", "device_kb"]
     assert [(r["variant"], int(r["k"])) for r in rows] == [
-        ("standard", 50), ("two-pass", 50), ("standard", 100), ("two-pass", 100)]
-    assert all(float(r["time_s"]) > 0 for r in rows)
+        ("standard", 50), ("standard", 100), ("standard", 150),
+        ("two-pass", 50), ("two-pass", 100), ("two-pass", 150)]
+    assert all(float(r["time_s"]) > 0 and int(r["rss_kb"]) > 0 for r in rows)
+    dev = {(r["variant"], int(r["k"])): int(r["device_kb"]) for r in rows}
+    n = 5115
+    for k in (50, 100, 150):
+        basis_kb = 8 * n * k // 1024
+        assert dev[("standard", k)] - dev[("two-pass", k)] >= basis_kb - 64
+    # two-pass: only the k-sized solver state grows (a few KB)
+    assert dev[("two-pass", 150)] - dev[("two-pass", 50)] < 64
+
+
+def test_scalability_rows(tmp_path):
+    """src/bin/scalability.rs schema, fresh worker per variant, two instances."""
+    from tpl_amd import harness
+    out = str(tmp_path / "s.csv")
+    harness.main(["scalability", "--arcs", "5000", "50000", "--k", "100", "--output", out])
+    with open(out) as f:
+        rows = list(csv.DictReader(f))
+    assert list(rows[0].keys()) == ["variant", "n", "k", "time_s", "rss_kb", "device_kb"]
+    assert [(r["variant"], int(r["n"])) for r in rows] == [
+        ("standard", 5115), ("standard", 50365), ("two-pass", 5115), ("two-pass", 50365)]
+    d = {(r["variant"], int(r["n"])): int(r["device_kb"]) for r in rows}
+    assert d[("standard", 50365)] - d[("two-pass", 50365)] >= 8 * 50365 * 100 // 1024 - 64

@@ -316,20 +316,53 @@ def test_error_semantics(op5k, kkt5k):
     assert e.value.kind == LanczosErrorKind.INPUT_ERROR
 
 
-def test_step_callback(op5k, kkt5k):
-    """LanczosCallback (src/algorithms/mod.rs:82-86, lanczos.rs:93-106): early stop."""
-    b = std_rng_vector(kkt5k.a.shape[0])
+@pytest.mark.parametrize("stop", [1, 2, 3, 7, 8, 31, 40])
+def test_step_callback(stop, op5k, kkt5k):
+    """LanczosCallback (src/algorithms/mod.rs:82-86, lanczos.rs:93-106): the callback sees
+    every step in order with the reference's TridiagonalSystemView and V view, and an
+    early stop at `stop` returns exactly the `stop`-step decomposition and basis — checked
+    against the canonical oracle (the host polls in batches of 1, 2, 4, ... 32 steps, so
+    stops fall inside and at the edges of batches)."""
+    a = kkt5k.a
+    n = a.shape[0]
+    b = std_rng_vector(n)
     seen = []
 
     def cb(k, v_view, t):
         seen.append((k, len(t.alphas), len(t.betas), v_view.shape))
-        return k < 7
-    out = alg.lanczos_standard(op5k, b, 20, callback=cb)
+        return k < stop
+    out = alg.lanczos_standard(op5k, b, 50, callback=cb)
+    assert out.decomposition.steps_taken == stop
+    assert [s[0] for s in seen] == list(range(1, stop + 1))
+    assert seen[-1] == (stop, stop, stop - 1, (n, stop))
+    al, be, steps, bn, V = canon(op5k, a).pass_one(b, stop, store_basis=True)
+    assert steps == stop
+    assert np.array_equal(out.decomposition.alphas, al[:stop])
+    assert np.array_equal(out.decomposition.betas, be[:stop - 1])
+    assert np.array_equal(np.asarray(out.v_k), V[:, :stop])
+
+
+def test_step_callback_views_and_exception(op5k, kkt5k):
+    """The T view at step k holds the first k alphas / k-1 betas of the final run; an
+    exception raised by the callback stops the loop and propagates to the caller."""
+    b = std_rng_vector(kkt5k.a.shape[0])
+    views = []
+    alg.lanczos_standard(op5k, b, 20, callback=lambda k, v, t: views.append(
+        (t.alphas.copy(), t.betas.copy())) or True)
     full = alg.lanczos_standard(op5k, b, 20)
-    assert out.decomposition.steps_taken == 7
-    assert seen[-1] == (7, 7, 6, (kkt5k.a.shape[0], 7))
-    assert np.array_equal(out.decomposition.alphas, full.decomposition.alphas[:7])
-    assert np.array_equal(out.v_k, full.v_k[:, :7])
+    for k, (va, vb) in enumerate(views, start=1):
+        assert np.array_equal(va, full.decomposition.alphas[:k])
+        assert np.array_equal(vb, full.decomposition.betas[:k - 1])
+
+    class Boom(Exception):
+        pass
+
+    def bad(k, v, t):
+        if k == 5:
+            raise Boom("stop here")
+        return True
+    with pytest.raises(Boom):
+        alg.lanczos_standard(op5k, b, 20, callback=bad)
 
 
 ACC_ROWS = {("inv", "well"): [10, 50, 100, 200], ("inv", "ill"): [10, 60, 120],

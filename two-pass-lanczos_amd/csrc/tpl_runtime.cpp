@@ -415,8 +415,15 @@ enum GraphKind {
   kGDevFtk = 5,       // (timed variant) device f(T_k) + pass-two prologue
   kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
 };
+// Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
+// run ahead of the host callback.
+constexpr int kCbBatchMax = 32;
 // One-graph solves keep the device f(T_k)'s working rows in LDS (6 k doubles, at most 64 KiB).
 constexpr size_t kDevFtkMaxK = 1365;
+// Auto mode: the device solve is one dependent chain of ~2 k fp64 divisions on one lane
+// (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
+// ~15-25 us (sync, host solve, upload, launch): one graph pays up to k ~ 128.
+constexpr size_t kDevFtkAutoK = 128;
 }
 
 struct tpl_op_s {
@@ -473,10 +480,13 @@ struct tpl_op_s {
   double* d_V = nullptr;    // standard-variant basis (n x vcols, ld = n)
   size_t vcols = 0;
   std::map<std::pair<int, size_t>, hipGraphExec_t> graphs;
+  // device allocations of this operator (pointer -> bytes): tpl_op_device_bytes
+  std::map<const void*, size_t> allocs;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // live timing (tpl_op_enable_timing): events recorded inside the captured passes
   bool timing = false;
-  bool device_ftk = true;           // built-in inv evaluated on the device (one-graph solve)
+  int device_ftk = 2;               // built-in inv on the device (one graph): 0 off, 1 on, 2 auto
+  bool last_one_graph = false;      // the last tpl_lanczos_two_pass ran as one device graph
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
 };
@@ -539,12 +549,25 @@ void drop_graphs(tpl_op_s* op) {
   op->graphs.clear();
 }
 
+// Device memory of an operator, accounted per allocation (tpl_op_device_bytes).
 template <class T>
-void upload(T** dst, const std::vector<T>& src) {
-  if (*dst) HIPCHK(hipFree(*dst));
-  *dst = nullptr;
+void dev_alloc(tpl_op_s* op, T** p, size_t bytes) {
+  HIPCHK(hipMalloc(p, bytes));
+  op->allocs[*p] = bytes;
+}
+template <class T>
+void dev_free(tpl_op_s* op, T*& p) {
+  if (!p) return;
+  op->allocs.erase(p);
+  hipFree(p);
+  p = nullptr;
+}
+
+template <class T>
+void upload(tpl_op_s* op, T** dst, const std::vector<T>& src) {
+  dev_free(op, *dst);
   if (src.empty()) return;
-  HIPCHK(hipMalloc(dst, src.size() * sizeof(T)));
+  dev_alloc(op, dst, src.size() * sizeof(T));
   HIPCHK(hipMemcpy(*dst, src.data(), src.size() * sizeof(T), hipMemcpyHostToDevice));
 }
 
@@ -559,33 +582,33 @@ void rebuild_schedule(tpl_op_s* op) {
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, op->h_rowptr, op->h_col,
                          op->h_val, op->sp, cmap);
   const Layout& L = op->lay;
-  upload(&op->d_srows, L.srows);
+  upload(op, &op->d_srows, L.srows);
   if (L.s_col16)
-    upload(reinterpret_cast<uint16_t**>(&op->d_scol), L.s_col16v);
+    upload(op, reinterpret_cast<uint16_t**>(&op->d_scol), L.s_col16v);
   else
-    upload(reinterpret_cast<int32_t**>(&op->d_scol), L.s_col);
-  upload(&op->d_scbase, L.s_cbase);
+    upload(op, reinterpret_cast<int32_t**>(&op->d_scol), L.s_col);
+  upload(op, &op->d_scbase, L.s_cbase);
   if (L.val_i8)
-    upload(reinterpret_cast<int8_t**>(&op->d_sval), L.s_val8);
+    upload(op, reinterpret_cast<int8_t**>(&op->d_sval), L.s_val8);
   else
-    upload(reinterpret_cast<double**>(&op->d_sval), L.s_val);
-  upload(&op->d_cbase, L.c_base);
-  upload(&op->d_cwidth, L.c_width);
+    upload(op, reinterpret_cast<double**>(&op->d_sval), L.s_val);
+  upload(op, &op->d_cbase, L.c_base);
+  upload(op, &op->d_cwidth, L.c_width);
   if (L.b_col16)
-    upload(reinterpret_cast<uint16_t**>(&op->d_bcol), L.b_col16v);
+    upload(op, reinterpret_cast<uint16_t**>(&op->d_bcol), L.b_col16v);
   else
-    upload(reinterpret_cast<int32_t**>(&op->d_bcol), L.b_col);
-  upload(&op->d_bcbase, L.b_cbase);
+    upload(op, reinterpret_cast<int32_t**>(&op->d_bcol), L.b_col);
+  upload(op, &op->d_bcbase, L.b_cbase);
   if (L.val_i8)
-    upload(reinterpret_cast<int8_t**>(&op->d_bval), L.b_val8);
+    upload(op, reinterpret_cast<int8_t**>(&op->d_bval), L.b_val8);
   else
-    upload(reinterpret_cast<double**>(&op->d_bval), L.b_val);
-  upload(&op->d_bseg, L.b_seg);
-  upload(&op->d_bhdr, L.b_hdr);
+    upload(op, reinterpret_cast<double**>(&op->d_bval), L.b_val);
+  upload(op, &op->d_bseg, L.b_seg);
+  upload(op, &op->d_bhdr, L.b_hdr);
   // piece slots, and the arrival counters of the sliced long rows (zero; they run on
   // modulo the slice count across launches)
-  upload(&op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlices, 1), 0.0));
-  upload(&op->d_Pcnt,
+  upload(op, &op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlices, 1), 0.0));
+  upload(op, &op->d_Pcnt,
          std::vector<unsigned int>(std::max<size_t>(L.lrows.size() * kCntStride, 1), 0u));
   drop_graphs(op);
   // partial buffers depend on the layout: force state reallocation
@@ -597,16 +620,16 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
   if (k > op->kcap) {
     const size_t kc = std::max<size_t>(k, 16);
     drop_graphs(op);
-    if (op->d_state) HIPCHK(hipFree(op->d_state));
+    dev_free(op, op->d_state);
     if (op->h_state) HIPCHK(hipHostFree(op->h_state));
-    if (op->d_Pr) HIPCHK(hipFree(op->d_Pr));
+    dev_free(op, op->d_Pr);
     op->d_state = nullptr;
     op->h_state = nullptr;
     op->d_Pr = nullptr;
     const CsrDev A = csr_dev(op);
     const size_t doubles = (kc + 1) + 3 * kc + (size_t)std::max(A.NA, 1) + (size_t)A.G2;
     const size_t bytes = 16 + doubles * sizeof(double);
-    HIPCHK(hipMalloc(&op->d_state, bytes));
+    dev_alloc(op, &op->d_state, bytes);
     HIPCHK(hipMemset(op->d_state, 0, bytes));
     HIPCHK(hipHostMalloc(&op->h_state, 16 + (4 * kc + 1) * sizeof(double), hipHostMallocDefault));
     char* base = (char*)op->d_state;
@@ -623,18 +646,18 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
   }
   if (reorth && !op->d_Pr) {
     // [cols x G partials][cols coefficients]
-    HIPCHK(hipMalloc(&op->d_Pr, ((size_t)op->lay.G2 + 1) * op->kcap * sizeof(double)));
+    dev_alloc(op, &op->d_Pr, ((size_t)op->lay.G2 + 1) * op->kcap * sizeof(double));
   }
 }
 
 void ensure_basis(tpl_op_s* op, size_t cols) {
   if (cols <= op->vcols && op->d_V) return;
   drop_graphs(op);
-  if (op->d_V) HIPCHK(hipFree(op->d_V));
+  dev_free(op, op->d_V);
   op->d_V = nullptr;
   op->vcols = 0;
   const size_t c = std::max<size_t>(cols, 1);
-  HIPCHK(hipMalloc(&op->d_V, (size_t)op->n * c * sizeof(double) + 64));
+  dev_alloc(op, &op->d_V, (size_t)op->n * c * sizeof(double) + 64);
   op->vcols = c;
 }
 
@@ -987,10 +1010,13 @@ void init_op(tpl_op_s* op) {
   if (op->dist && !op->hybrid)
     for (int r = 0; r < R; ++r) widest = std::max(widest, op->starts[r + 1] - op->starts[r]);
   op->ld = ((std::max<int64_t>(widest, 1) + 63) / 64) * 64;
+  // gathered column indices (ColMap: r * ld + local) are int32 on the device
+  if ((int64_t)R * op->ld >= (int64_t)INT32_MAX)
+    fail(TPL_ERR_UNSUPPORTED, "row blocks too unbalanced: nranks x widest block >= 2^31");
   rebuild_schedule(op);
   // gathered: b, R0..2, V2_0..2, tmp (R x ld each); local: W, x (ld each)
   const size_t gathered = 8 * (size_t)R * op->ld, local = 2 * (size_t)op->ld;
-  HIPCHK(hipMalloc(&op->d_vecs, (gathered + local) * sizeof(double)));
+  dev_alloc(op, &op->d_vecs, (gathered + local) * sizeof(double));
   HIPCHK(hipMemset(op->d_vecs, 0, (gathered + local) * sizeof(double)));
   double* p = op->d_vecs;
   const size_t gl = (size_t)R * op->ld;
@@ -1012,11 +1038,11 @@ void init_op(tpl_op_s* op) {
     // [nranks alpha totals | long-row alpha partials (hybrid) | nranks norm totals]
     const size_t nr = (size_t)op->dist->nranks;
     const size_t cnt = 2 * nr + (op->hybrid ? (size_t)long_epi_blocks(op) : 0);
-    HIPCHK(hipMalloc(&op->d_rsum, cnt * sizeof(double)));
+    dev_alloc(op, &op->d_rsum, cnt * sizeof(double));
     HIPCHK(hipMemset(op->d_rsum, 0, cnt * sizeof(double)));
     if (op->hybrid) {
       const size_t ya = std::max<size_t>(nr * op->lay.lrows.size(), 1);
-      HIPCHK(hipMalloc(&op->d_yall, ya * sizeof(double)));
+      dev_alloc(op, &op->d_yall, ya * sizeof(double));
       HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
     }
   }
@@ -1155,7 +1181,7 @@ int64_t tpl_op_nrows(tpl_op_t op) { return op ? op->n : -1; }
 int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
   return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0) |
-         (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0);
+         (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0) | (op->last_one_graph ? 32 : 0);
 }
 
 tpl_status tpl_op_set_value_format(tpl_op_t op, int compress) {
@@ -1222,21 +1248,44 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
       run_pass_one(op, b, k, mem, true, reorth != 0);
       d = fetch_decomp(op, k);
     } else {
-      // Slow path mirroring src/algorithms/lanczos.rs:86-128 with a host callback per step.
+      // src/algorithms/lanczos.rs:86-128 with the host callback after every step, polled
+      // in batches: the device runs a batch of steps ahead (1, 2, 4, ... up to
+      // kCbBatchMax steps: at most as many speculative steps as were already confirmed),
+      // then the callback sees steps j = first .. last of the batch in order, each with
+      // the T_j view of that step (alphas[0..j), betas[0..j-1)) and V's first j columns.
+      // A stop at step j truncates the decomposition to j steps: later steps never change
+      // earlier alphas, betas or columns, so the result is exactly the one-step-at-a-time
+      // result, with one host synchronisation per batch instead of per step.
       ensure_state(op, k, reorth != 0);
       ensure_basis(op, k);
       upload_vec(op, op->b, b, mem);
       enqueue_p1_prologue(op);
-      for (int j = 1; j <= (int)k; ++j) {
-        enqueue_p1_step(op, j, (int)k, op->d_V + (size_t)(j - 1) * op->n);
+      size_t stop_at = k;
+      int batch = 1;
+      for (int j0 = 1; j0 <= (int)k;) {
+        const int j1 = std::min<int>((int)k, j0 + batch - 1);
+        for (int j = j0; j <= j1; ++j) {
+          enqueue_p1_step(op, j, (int)k, op->d_V + (size_t)(j - 1) * op->n);
+          if (reorth && j < (int)k) enqueue_reorth(op, j);
+        }
         d = fetch_decomp(op, k);
-        if (d.flags[0] || d.steps < (size_t)j) break; // zero b or breakdown before step j
-        const int go = cb((size_t)j, op->d_V, op->n, d.alphas, d.steps, d.betas,
-                          d.steps > 0 ? d.steps - 1 : 0, cb_user);
+        bool go = true;
+        for (int j = j0; j <= j1 && go; ++j) {
+          if (d.flags[0] && d.steps < (size_t)j) {  // zero b, or breakdown before step j
+            stop_at = d.steps;
+            go = false;
+            break;
+          }
+          go = cb((size_t)j, op->d_V, op->n, d.alphas, (size_t)j, d.betas, (size_t)j - 1,
+                  cb_user) != 0;
+          if (!go) stop_at = (size_t)j;
+        }
         if (!go) break;
-        if (reorth && j < (int)k) enqueue_reorth(op, j);
+        j0 = j1 + 1;
+        batch = std::min(2 * batch, kCbBatchMax);
       }
       d = fetch_decomp(op, k);
+      d.steps = std::min(d.steps, stop_at);
     }
     if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
     std::memcpy(alphas, d.alphas, d.steps * sizeof(double));
@@ -1300,11 +1349,13 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
     set_device(op);
     check_b(op, b, b_len);
     check_k(k);
-    if (f == &tpl_ftk_inv && op->device_ftk && !op->dist && k <= kDevFtkMaxK) {
+    const size_t kmax = op->device_ftk == 1 ? kDevFtkMaxK : op->device_ftk == 2 ? kDevFtkAutoK : 0;
+    if (f == &tpl_ftk_inv && !op->dist && k <= kmax) {
       // one graph: pass one, y = ||b|| T^{-1} e_1 on the device, pass two (the built-in
       // inv is the same computation as on the host, bit for bit; src/solvers.rs:148-174)
       ensure_state(op, k);
       upload_vec(op, op->b, b, mem);
+      op->last_one_graph = true;
       run_two_pass_dev(op, k);
       download_vec(op, x_out, op->x, op->n, mem);
       HIPCHK(hipMemcpyAsync(op->h_state, op->d_state, 16, hipMemcpyDeviceToHost, op->stream));
@@ -1316,6 +1367,7 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
       return;
     }
     // 1. pass one (src/solvers.rs:148)
+    op->last_one_graph = false;
     run_pass_one(op, b, k, mem, false, false);
     const HostDecomp d = fetch_decomp(op, k);
     if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
@@ -1433,10 +1485,20 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
   }
 }
 
-tpl_status tpl_op_set_device_ftk(tpl_op_t op, int on) {
+tpl_status tpl_op_device_bytes(tpl_op_t op, uint64_t* bytes) {
+  return guarded([&] {
+    if (!op || !bytes) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    uint64_t t = 0;
+    for (const auto& kv : op->allocs) t += kv.second;
+    *bytes = t;
+  });
+}
+
+tpl_status tpl_op_set_device_ftk(tpl_op_t op, int mode) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
-    op->device_ftk = on != 0;
+    if (mode < 0 || mode > 2) fail(TPL_ERR_INVALID_ARGUMENT, "device f(T_k) mode must be 0, 1 or 2");
+    op->device_ftk = mode;
   });
 }
 

@@ -100,6 +100,7 @@ def lanczos_standard(operator, b, k: int, callback: Optional[Callable] = None,
     bnorm = c_double(0.0)
     v_full = bv.empty(max(k, 1), op.nrows())  # C-order (k, n) == column-major (n, k)
     cb_c = None
+    raised = []
     if callback is not None:
         def _cb(kk, vptr, n, pa, na, pb, nb, user):
             va = np.ctypeslib.as_array(pa, (na,)).copy() if na else np.zeros(0)
@@ -107,13 +108,16 @@ def lanczos_standard(operator, b, k: int, callback: Optional[Callable] = None,
             try:
                 return 1 if callback(int(kk), DeviceBasisView(vptr, int(n), int(kk)),
                                      TridiagonalSystemView(va, vb, int(kk))) else 0
-            except Exception:
+            except BaseException as e:  # stop the device loop, re-raised below
+                raised.append(e)
                 return 0
         cb_c = _lib.STEP_CB(_cb)
     check(_lib.tpl_lanczos_standard(
         op.handle, bv.ptr, bv.n, k, alphas.ctypes.data_as(POINTER(c_double)),
         betas.ctypes.data_as(POINTER(c_double)), byref(steps), byref(bnorm), Vec.ptr_of(v_full),
         bv.mem, 1 if reorthogonalize else 0, cb_c, None))
+    if raised:
+        raise raised[0]
     s = steps.value
     v_k = v_full[:s].T
     dec = LanczosDecomposition(alphas[:s].copy(), betas[:max(s - 1, 0)].copy(), s, bnorm.value)

@@ -1,8 +1,8 @@
 """Experiment harness on the MI355X engine — the callers of the hot path in the
 reference's binaries, with the same inputs, sweeps and CSV schemas:
 
-  tradeoff      src/bin/tradeoff.rs      variant,k,time_s,rss_kb          (KKT instance, f = inv)
-  scalability   src/bin/scalability.rs   variant,n,k,time_s,rss_kb        (several instances, f = inv)
+  tradeoff      src/bin/tradeoff.rs      variant,k,time_s,rss_kb,device_kb   (KKT instance, f = inv)
+  scalability   src/bin/scalability.rs   variant,n,k,time_s,rss_kb,device_kb (several instances)
   accuracy      src/bin/stability.rs     k,relative_error_standard,relative_error_two_pass,
                                          relative_solution_deviation      (diagonal spectra)
   orthogonality src/bin/orthogonality.rs k,ortho_loss_standard,ortho_loss_regenerated,
@@ -11,18 +11,30 @@ reference's binaries, with the same inputs, sweeps and CSV schemas:
     python -m tpl_amd.harness tradeoff --arcs 500000 --output tradeoff.csv
     python -m tpl_amd.harness accuracy --function inv --scenario well-conditioned --output a.csv
 
-time_s is the wall time of one solver call with b and x in host memory (the
-reference's window, src/bin/tradeoff.rs:265-288); rss_kb is the process's peak host
-RSS (the basis lives in HBM here, so it does not show in RSS). f(T_k) uses the engine's
-built-in solvers: inv = tridiagonal LU (the harness's sp_lu), exp = symmetric
-tridiagonal eigensolver (self_adjoint_eigen).
+tradeoff / scalability follow the reference's orchestrator (src/bin/tradeoff.rs:160-214,
+src/bin/scalability.rs:120-215): every variant runs in a FRESH worker process (this
+module re-run with TPL_HARNESS_VARIANT set) that prints its CSV rows, so one variant's
+allocations never show in the other's numbers. Per k the worker first makes one
+untimed call (the engine's one-time work at a new k: growing the state / basis,
+capturing and instantiating the k-step graphs), then times one call with b and x in
+host memory (the reference's window, src/bin/tradeoff.rs:265-288).
+  rss_kb    : VmPeak of the worker (/proc/self/status), exactly the reference's
+              get_peak_rss_kb (src/utils/perf.rs:16-31) — host memory;
+  device_kb : device memory the operator holds after the call (tpl_op_device_bytes):
+              layout + recurrence vectors + state, plus V_k (8 n k bytes) for the
+              standard variant. This is where the reference's memory trade-off lives on
+              this engine (results/scalability_k500_rho3.csv: 2,090,524 vs 194,472 KB).
+f(T_k) uses the engine's built-in solvers: inv = tridiagonal LU (the harness's sp_lu),
+exp = symmetric tridiagonal eigensolver (self_adjoint_eigen).
 """
 from __future__ import annotations
 
 import argparse
 import csv
+import io
 import os
-import resource
+import subprocess
+import sys
 import time
 
 import numpy as np
@@ -37,7 +49,18 @@ VARIANTS = ("standard", "two-pass")
 
 
 def _rss_kb() -> int:
-    return int(resource.getrusage(resource.RUSAGE_SELF).ru_maxrss)
+    """VmPeak (kB) of this process, as src/utils/perf.rs:16-31 reads it (0 if unreadable)."""
+    try:
+        with open("/proc/self/status") as f:
+            for line in f:
+                if line.startswith("VmPeak:"):
+                    return int(line.split()[1])
+    except OSError:
+        pass
+    return 0
+
+
+VARIANT_ENV = "TPL_HARNESS_VARIANT"
 
 
 def _solve(variant, op, b, k, f):
@@ -61,34 +84,57 @@ def kkt_instance(arcs: int | None = None, dmx: str | None = None, qfc: str | Non
     return a, a @ np.full(a.shape[0], 1.0 / np.sqrt(a.shape[0]))
 
 
-def tradeoff(a, b, ks, device: int = 0):
-    """Rows (variant, k, time_s, rss_kb) for every k (src/bin/tradeoff.rs:262-300)."""
+def _timed(variant, op, b, k):
+    """One untimed call at k (one-time work), then one timed call -> (time_s, rss_kb,
+    device_kb)."""
+    _solve(variant, op, b, k, "inv")
+    t0 = time.perf_counter()
+    _solve(variant, op, b, k, "inv")
+    dt = time.perf_counter() - t0
+    return dt, _rss_kb(), op.device_bytes() // 1024
+
+
+def tradeoff_worker(variant, a, b, ks, device: int = 0):
+    """Rows (variant, k, time_s, rss_kb, device_kb) of ONE variant, k ascending
+    (src/bin/tradeoff.rs:222-300, run_worker)."""
     op = HipCsrOp(a, device=device)
-    _solve("two-pass", op, b, min(ks), "inv")  # warm-up: layout, graphs, clocks
     rows = []
     for k in ks:
-        for v in VARIANTS:
-            t0 = time.perf_counter()
-            _solve(v, op, b, k, "inv")
-            rows.append({"variant": v, "k": k, "time_s": time.perf_counter() - t0,
-                         "rss_kb": _rss_kb()})
+        t, rss, dev = _timed(variant, op, b, k)
+        rows.append({"variant": variant, "k": k, "time_s": t, "rss_kb": rss, "device_kb": dev})
+    op.close()
     return rows
 
 
-def scalability(instances, k: int = 500, device: int = 0):
-    """Rows (variant, n, k, time_s, rss_kb), one instance after another
-    (src/bin/scalability.rs)."""
+def scalability_worker(variant, instances, k: int = 500, device: int = 0):
+    """Rows (variant, n, k, time_s, rss_kb, device_kb) of ONE variant over the instances."""
     rows = []
     for a, b in instances:
         op = HipCsrOp(a, device=device)
-        _solve("two-pass", op, b, min(k, 10), "inv")
-        for v in VARIANTS:
-            t0 = time.perf_counter()
-            _solve(v, op, b, k, "inv")
-            rows.append({"variant": v, "n": a.shape[0], "k": k,
-                         "time_s": time.perf_counter() - t0, "rss_kb": _rss_kb()})
+        t, rss, dev = _timed(variant, op, b, k)
+        rows.append({"variant": variant, "n": a.shape[0], "k": k, "time_s": t, "rss_kb": rss,
+                     "device_kb": dev})
         op.close()
     return rows
+
+
+def run_workers(argv, fields):
+    """Orchestrator: this module once per variant in a fresh process (env VARIANT_ENV),
+    each printing headerless CSV rows; returns the rows in variant order."""
+    rows = []
+    for v in VARIANTS:
+        env = dict(os.environ, **{VARIANT_ENV: v})
+        out = subprocess.run([sys.executable, "-m", "tpl_amd.harness"] + list(argv), env=env,
+                             check=True, capture_output=True, text=True,
+                             cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        for rec in csv.reader(io.StringIO(out.stdout)):
+            if rec:
+                rows.append(dict(zip(fields, rec)))
+    return rows
+
+
+TRADEOFF_FIELDS = ["variant", "k", "time_s", "rss_kb", "device_kb"]
+SCALABILITY_FIELDS = ["variant", "n", "k", "time_s", "rss_kb", "device_kb"]
 
 
 def diagonal_problem(n: int, function: str, scenario: str):
@@ -191,11 +237,23 @@ def main(argv=None):
         q.add_argument("--k-step", type=int, default=10 if name == "accuracy" else 20)
         q.add_argument("--output", required=True)
     a = p.parse_args(argv)
+    argv = list(sys.argv[1:] if argv is None else argv)
+    worker = os.environ.get(VARIANT_ENV)
+    if a.cmd in ("tradeoff", "scalability") and worker:
+        if a.cmd == "tradeoff":
+            A, b = kkt_instance(a.arcs, a.dmx, a.qfc, fixtures)
+            rows = tradeoff_worker(worker, A, b, list(range(a.k_start, a.k_end + 1, a.k_step)))
+        else:
+            rows = scalability_worker(worker, [kkt_instance(m, fixtures=fixtures) for m in a.arcs],
+                                      a.k)
+        w = csv.writer(sys.stdout)
+        for r in rows:
+            w.writerow(list(r.values()))
+        return
     if a.cmd == "tradeoff":
-        A, b = kkt_instance(a.arcs, a.dmx, a.qfc, fixtures)
-        rows = tradeoff(A, b, list(range(a.k_start, a.k_end + 1, a.k_step)))
+        rows = run_workers(argv, TRADEOFF_FIELDS)
     elif a.cmd == "scalability":
-        rows = scalability([kkt_instance(m, fixtures=fixtures) for m in a.arcs], a.k)
+        rows = run_workers(argv, SCALABILITY_FIELDS)
     elif a.cmd == "accuracy":
         rows = accuracy(a.function, a.scenario, a.n, a.k_min, a.k_max, a.k_step)
     else:

@@ -47,8 +47,10 @@ def _as_csr_arrays(a):
     import scipy.sparse as sp
     if not sp.issparse(a):
         a = sp.csr_matrix(np.asarray(a, dtype=np.float64))
-    m = a.tocsr()
-    m.sort_indices()
+    # a private copy: the caller's matrix is never modified; duplicates are summed and
+    # columns sorted (faer's try_new_from_triplets semantics), explicit zeros are kept
+    m = a.tocsr(copy=True)
+    m.sum_duplicates()
     if m.shape[0] != m.shape[1]:
         raise TplError(_lib.TPL_ERR_INVALID_ARGUMENT, "operator must be square")
     return (m.shape[0], m.indptr.astype(np.int64), m.indices.astype(np.int32),
@@ -149,10 +151,20 @@ class HipCsrOp:
         check(_lib.tpl_profile_kernel(self._op, kernel, iters, byref(us), byref(by)))
         return us.value, by.value
 
-    def set_device_ftk(self, on: bool = True):
-        """Built-in inv of lanczos_two_pass evaluated on the device, the solve as one graph
-        (default), or on the host between the passes."""
-        check(_lib.tpl_op_set_device_ftk(self._op, 1 if on else 0))
+    def flags(self) -> int:
+        """tpl_op_flags bits (include/tpl.h)."""
+        return int(_lib.tpl_op_flags(self._op))
+
+    def device_bytes(self) -> int:
+        """Device memory the operator holds (layout, vectors, state, V_k once allocated)."""
+        v = ctypes.c_uint64()
+        check(_lib.tpl_op_device_bytes(self._op, ctypes.byref(v)))
+        return int(v.value)
+
+    def set_device_ftk(self, mode=2):
+        """Built-in inv of lanczos_two_pass: 0 / False host (two graphs), 1 / True on the
+        device, the whole solve one graph, 2 auto (default: device for k <= 128)."""
+        check(_lib.tpl_op_set_device_ftk(self._op, int(mode)))
 
     def enable_timing(self, on: bool = True):
         """Record HIP events inside the captured passes of later solves."""
