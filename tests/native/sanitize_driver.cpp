@@ -1,0 +1,217 @@
+// sanitize_driver.cpp — the engine's host C++ (the .dmx/.qfc loader, the f(T_k) solvers,
+// the SpMV layout builder) built with -fsanitize=address,undefined on the CPU and driven
+// over the committed fixture, malformed and random inputs (sanitizers on
+// host code; tpl_loader.cpp parses untrusted files). Any sanitizer report aborts the run;
+// the layout checks also verify that every nonzero lands exactly once in the layout.
+//
+//   sanitize_driver <netgen-5000-3.dmx> <qfc> <scratch dir>
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "tpl.h"
+#include "tpl_internal.h"
+#include "tpl_layout.h"
+
+static int g_fail = 0;
+#define CHECK(cond, ...)                                \
+  do {                                                  \
+    if (!(cond)) {                                      \
+      std::printf("FAIL %s:%d: ", __FILE__, __LINE__);  \
+      std::printf(__VA_ARGS__);                         \
+      std::printf("\n");                                \
+      ++g_fail;                                         \
+    }                                                   \
+  } while (0)
+
+static void write_file(const std::string& path, const std::string& text) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  std::fwrite(text.data(), 1, text.size(), f);
+  std::fclose(f);
+}
+
+static void loader_checks(const char* dmx, const char* qfc, const std::string& dir) {
+  tpl_csr_host A{};
+  CHECK(tpl_load_kkt_system(dmx, qfc, &A) == TPL_OK, "fixture: %s", tpl_last_error());
+  CHECK(A.n == 5115 && A.nnz == 20000, "fixture sizes");
+  tpl_csr_host_free(&A);
+  // malformed inputs: every one must fail cleanly (status + message), never crash
+  const char* bad[][2] = {
+      {"p min 2 1\na 0 1\n", "1\n"},   {"a 1 2\n", "1\n"},          {"p min 2 1\na 1 x\n", "1\n"},
+      {"p min 2 1\na 1 2\n", "2\n"},   {"p min 2 1\na 1 2\n", ""},  {"p min 2 1\na 1 99999999999\n", "1\n"},
+      {"p min 2 1\na 1 2\n", "1\n1\nabc\n"}, {"p min -5 -1\n", "1\n"}, {"p min 2 1\na 1\n", "1\n"},
+      {"p min 3 2\na 1 2\na 3 -1\n", "2\n"}, {"p min 2 1\na 2 1\na 1 2\n", "2\n"},
+  };
+  for (auto& t : bad) {
+    write_file(dir + "/m.dmx", t[0]);
+    write_file(dir + "/m.qfc", t[1]);
+    tpl_csr_host B{};
+    const tpl_status st = tpl_load_kkt_system((dir + "/m.dmx").c_str(), (dir + "/m.qfc").c_str(), &B);
+    if (st == TPL_OK) tpl_csr_host_free(&B);
+    else CHECK(std::strlen(tpl_last_error()) > 0, "error without message");
+  }
+  // random mutations of small valid files
+  std::mt19937_64 rng(7);
+  const std::string good = "c x\np min 4 5\na 1 2 0 1 1\na 2 3 0 1 2\na 3 4 0 1 3\na 4 1 0 1 4\na 1 3 0 1 5\n";
+  const std::string qgood = "5\n1\n2\n3\n4\n5\n0.5\n1.5\n2.5\n3.5\n4.5\n";
+  const char alphabet[] = "0123456789 -+.eExap\n\tmin";
+  for (int it = 0; it < 400; ++it) {
+    std::string d = good, q = qgood;
+    const int edits = 1 + (int)(rng() % 6);
+    for (int e = 0; e < edits; ++e) {
+      std::string& s = (rng() % 3 == 0) ? q : d;
+      if (s.empty()) continue;
+      const size_t pos = rng() % s.size();
+      switch (rng() % 3) {
+        case 0: s[pos] = alphabet[rng() % (sizeof alphabet - 1)]; break;
+        case 1: s.erase(pos, 1 + rng() % 4); break;
+        default: s.insert(pos, 1, alphabet[rng() % (sizeof alphabet - 1)]);
+      }
+    }
+    write_file(dir + "/r.dmx", d);
+    write_file(dir + "/r.qfc", q);
+    tpl_csr_host B{};
+    if (tpl_load_kkt_system((dir + "/r.dmx").c_str(), (dir + "/r.qfc").c_str(), &B) == TPL_OK) {
+      for (int64_t i = 0; i < B.n; ++i) CHECK(B.row_ptr[i] <= B.row_ptr[i + 1], "row_ptr");
+      for (int64_t q2 = 0; q2 < B.nnz; ++q2) CHECK(B.col_idx[q2] >= 0 && B.col_idx[q2] < B.n, "col");
+      tpl_csr_host_free(&B);
+    }
+  }
+  tpl_csr_host G{};
+  CHECK(tpl_generate_kkt(3000, 80, 11, &G) == TPL_OK, "generate");
+  tpl_csr_host_free(&G);
+  CHECK(tpl_generate_kkt(0, 80, 11, &G) != TPL_OK, "generate: bad sizes accepted");
+}
+
+static void ftk_checks() {
+  std::mt19937_64 rng(3);
+  std::uniform_real_distribution<double> U(-2.0, 2.0);
+  for (size_t k : {1, 2, 3, 10, 57, 200, 333}) {
+    std::vector<double> a(k), b(k > 1 ? k - 1 : 0), y(k);
+    for (auto& v : a) v = U(rng);
+    for (auto& v : b) v = 0.1 + std::fabs(U(rng));
+    size_t len = 0;
+    char err[64];
+    for (auto fn : {tpl_ftk_inv, tpl_ftk_exp, tpl_ftk_sq}) {
+      const int rc = fn(a.data(), k, b.data(), b.size(), y.data(), k, &len, err, sizeof err, nullptr);
+      CHECK(rc == 0 && len == k, "ftk rc %d k %zu", rc, k);
+    }
+    // inv: residual of T y = e1
+    tpl_ftk_inv(a.data(), k, b.data(), b.size(), y.data(), k, &len, err, sizeof err, nullptr);
+    double r = 0, s = 0;
+    for (size_t i = 0; i < k; ++i) {
+      double t = a[i] * y[i] - (i == 0 ? 1.0 : 0.0);
+      if (i > 0) t += b[i - 1] * y[i - 1];
+      if (i + 1 < k) t += b[i] * y[i + 1];
+      r += t * t;
+      s += y[i] * y[i];
+    }
+    CHECK(std::sqrt(r) <= 1e-9 * std::max(1.0, std::sqrt(s)), "inv residual %g (k %zu)", std::sqrt(r), k);
+  }
+  // capacity errors write the message within err_cap
+  double a1[3] = {1, 2, 3}, y1[3];
+  size_t len = 0;
+  char tiny[4];
+  CHECK(tpl_ftk_exp(a1, 3, a1, 0, y1, 3, &len, tiny, sizeof tiny, nullptr) != 0 && tiny[3] == '\0',
+        "exp size error");
+}
+
+// Symmetric random matrix: `hubs` rows of `hub_len` entries, the rest short.
+static void random_csr(int64_t n, int hubs, int hub_len, uint64_t seed, std::vector<int32_t>& rp,
+                       std::vector<int32_t>& col, std::vector<double>& val) {
+  std::mt19937_64 rng(seed);
+  std::map<std::pair<int32_t, int32_t>, double> m;
+  for (int64_t i = 0; i < n; ++i) {
+    const int k = (int)(rng() % 4);
+    for (int e = 0; e < k; ++e) {
+      const int32_t j = (int32_t)(rng() % n);
+      const double v = (double)((int)(rng() % 5) - 2);
+      m[{(int32_t)i, j}] = v;
+      m[{j, (int32_t)i}] = v;
+    }
+  }
+  for (int h = 0; h < hubs && n > 1; ++h) {
+    const int32_t r = (int32_t)(rng() % n);
+    for (int e = 0; e < hub_len; ++e) {
+      const int32_t j = (int32_t)(rng() % n);
+      m[{r, j}] = 1.0;
+      m[{j, r}] = 1.0;
+    }
+  }
+  rp.assign(n + 1, 0);
+  col.clear();
+  val.clear();
+  for (auto& kv : m) rp[kv.first.first + 1]++;
+  for (int64_t i = 0; i < n; ++i) rp[i + 1] += rp[i];
+  for (auto& kv : m) {
+    col.push_back(kv.first.second);
+    val.push_back(kv.second);
+  }
+}
+
+static void layout_checks() {
+  struct Case { int64_t n; int hubs, hub_len; int slices, srm; bool compress; };
+  const Case cases[] = {{1, 0, 0, 0, -1, true},      {2, 1, 1, 0, -1, true},     {7, 1, 5, 0, -1, false},
+                        {1000, 3, 300, 0, -1, true}, {1000, 3, 300, 8, 2, false}, {20000, 2, 9000, 0, -1, true},
+                        {20000, 40, 700, 2, -1, true}, {5000, 0, 0, 4, 6, true}};
+  for (const Case& c : cases) {
+    std::vector<int32_t> rp, col;
+    std::vector<double> val;
+    random_csr(c.n, c.hubs, c.hub_len, 1234 + c.n, rp, col, val);
+    tpl::SchedParams sp;
+    sp.slices = c.slices;
+    sp.short_row_max = c.srm;
+    sp.compress_values = sp.compress_cols = c.compress;
+    tpl::Layout L;
+    try {
+      L = tpl::build_layout(c.n, c.n, rp, col, val, sp, tpl::ColMap{});
+    } catch (const tpl::Error& e) {
+      std::printf("FAIL layout n=%lld: %s\n", (long long)c.n, e.msg.c_str());
+      ++g_fail;
+      continue;
+    }
+    // every nonzero exactly once: short rows through the chunks, long rows through bins
+    CHECK((int64_t)(L.srows.size() + L.lrows.size()) == c.n, "row split");
+    int64_t seen_short = 0, seen_long = 0;
+    const bool c16 = L.s_col16, b16 = L.b_col16;
+    const int64_t nch = (int64_t)L.c_base.size();
+    for (int64_t ch = 0; ch < nch; ++ch)
+      for (int64_t k = 0; k < L.c_width[ch]; ++k)
+        for (int p = 0; p < tpl::kChunkRows; ++p) {
+          const int64_t e = L.c_base[ch] + k * tpl::kChunkRows + p;
+          const bool pad = c16 ? L.s_col16v[e] == 0xFFFF : L.s_col[e] < 0;
+          seen_short += !pad;
+        }
+    const size_t nbins = L.b_hdr.size();
+    for (size_t bin = 0; bin < nbins && !L.lrows.empty(); ++bin)
+      for (int32_t e = 0; e < L.bin_cap; ++e) {
+        const size_t q = bin * L.bin_cap + e;
+        const bool pad = b16 ? L.b_col16v[q] == 0xFFFF : L.b_col[q] < 0;
+        seen_long += !pad;
+      }
+    int64_t want_short = 0, want_long = 0;
+    for (int32_t r : L.srows) want_short += rp[r + 1] - rp[r];
+    for (int32_t r : L.lrows) want_long += rp[r + 1] - rp[r];
+    CHECK(seen_short == want_short && seen_long == want_long, "entries n=%lld: short %lld/%lld long %lld/%lld",
+          (long long)c.n, (long long)seen_short, (long long)want_short, (long long)seen_long,
+          (long long)want_long);
+  }
+}
+
+int main(int argc, char** argv) {
+  if (argc < 4) {
+    std::printf("usage: sanitize_driver <dmx> <qfc> <scratch dir>\n");
+    return 2;
+  }
+  loader_checks(argv[1], argv[2], argv[3]);
+  ftk_checks();
+  layout_checks();
+  std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "OK", g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,74 @@
+// tpl_layout.h — the SpMV layout of an operator (host side): short rows as sliced ELL,
+// long rows cut into column slices and packed into bins (tpl_device.h describes the
+// device view). Pure host code, built by tpl_layout.cpp; the runtime uploads the result.
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <vector>
+
+#include "tpl_device.h"
+
+namespace tpl {
+
+struct SchedParams {
+  int short_row_max = -1;           // rows longer than this are sliced; -1 = auto
+  int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
+  int64_t long_from = -1;           // >= 0: rows [long_from, n) are long, the rest short
+  bool compress_values = true;      // int8 values when all values are small integers
+  bool compress_cols = true;        // uint16 column offsets when the spans allow
+  int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
+};
+
+// Host copy of the SpMV layout (tpl_device.h).
+struct Layout {
+  std::vector<int32_t> srows;       // short rows, ascending
+  std::vector<int32_t> s_col;       // sliced ELL entries (col = -1: padding)
+  std::vector<double> s_val;
+  std::vector<int32_t> c_base, c_width;
+  int32_t s_width = 0;              // uniform chunk width (0: per-chunk)
+  int32_t s_identity = 0;
+  std::vector<int32_t> lrows;       // long rows, ascending
+  std::vector<int32_t> b_col;       // long-row bins: n_bins x bin_cap entries
+  std::vector<double> b_val;
+  bool val_i8 = false;              // every value a small integer: stored as int8
+  std::vector<int8_t> s_val8, b_val8;
+  bool s_col16 = false, b_col16 = false;  // uint16 column offsets from a per-chunk/bin base
+  std::vector<uint16_t> s_col16v, b_col16v;
+  std::vector<int32_t> s_cbase, b_cbase;
+  int32_t nslices = 1;              // column slices of the long rows
+  std::vector<BinSeg> b_seg;        // n_bins x kTPB table slots
+  std::vector<int32_t> b_hdr;       // per bin: pieces | long pieces << 16
+  int32_t bin_cap = kBinMin;
+  int32_t M = 0;                    // bins per slice
+  int G2 = 1;
+  int64_t E = 512;
+  int32_t s_win = 0, s_win_max = 0;  // short-chunk column window (tpl_device.h)
+};
+
+// Column index as stored on the device: the identity on one GPU; with the rows
+// partitioned over ranks, global column c (owned by rank r, rows [starts[r],
+// starts[r+1])) lives at r * ld + (c - starts[r]) of the all-gathered vector.
+struct ColMap {
+  const std::vector<int64_t>* starts = nullptr;  // row partition (nullptr: see table)
+  int64_t ld = 0;
+  int32_t operator()(int32_t c) const {
+    if (!starts) return c;
+    const auto it = std::upper_bound(starts->begin(), starts->end(), (int64_t)c);
+    const int64_t r = (it - starts->begin()) - 1;
+    return (int32_t)(r * ld + (c - (*starts)[r]));
+  }
+};
+
+// Short-row threshold: requested (> 0), or the auto rule T = clamp(2 * median row nnz,
+// 4, kShortRowMax).
+int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int requested);
+
+// n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds are
+// taken on global column indices, so a partition of one rank reproduces the single-GPU
+// layout exactly). Throws tpl::Error (TPL_ERR_UNSUPPORTED) for layouts the device
+// kernels cannot hold.
+Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
+                    const std::vector<int32_t>& col, const std::vector<double>& val,
+                    const SchedParams& sp, const ColMap& cmap);
+
+} // namespace tpl

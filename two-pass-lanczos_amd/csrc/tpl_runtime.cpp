@@ -24,6 +24,7 @@
 
 #include "tpl_device.h"
 #include "tpl_internal.h"
+#include "tpl_layout.h"
 
 namespace tpl {
 namespace launch {
@@ -57,26 +58,6 @@ hipError_t reorth_update(int64_t n, int cols, const double* V, double* r, const 
                          double* Pnorm, int G, int64_t E, hipStream_t s);
 } // namespace launch
 
-// ----------------------------------------------------------------- errors
-static thread_local std::string g_last_error;
-void set_last_error(const std::string& m) { g_last_error = m; }
-
-std::string msg_input(const std::string& what) { return "Invalid input parameter: " + what; }
-std::string msg_param_mismatch(const std::string& name, size_t expected, size_t actual) {
-  return "Parameter mismatch: `" + name + "` expects size " + std::to_string(expected) +
-         ", but got " + std::to_string(actual) + ".";
-}
-std::string msg_solver(const std::string& e) {
-  return "The user-provided f(T_k) solver failed: " + e;
-}
-std::string msg_dimension(int64_t operator_cols, int64_t vector_rows) {
-  return "Dimension mismatch: operator has " + std::to_string(operator_cols) +
-         " columns but vector has " + std::to_string(vector_rows) + " rows.";
-}
-std::string msg_evd(const std::string& e) {
-  return "A numerical error occurred during the eigendecomposition of T_k: " + e;
-}
-
 #define HIPCHK(expr)                                                                        \
   do {                                                                                      \
     hipError_t e_ = (expr);                                                                 \
@@ -89,303 +70,18 @@ template <class F>
 static tpl_status guarded(F&& f) {
   try {
     f();
-    g_last_error.clear();
+    set_last_error("");
     return TPL_OK;
   } catch (const Error& e) {
-    g_last_error = e.msg;
+    set_last_error(e.msg);
     return e.code;
   } catch (const std::bad_alloc&) {
-    g_last_error = "host allocation failed";
+    set_last_error("host allocation failed");
     return TPL_ERR_OUT_OF_MEMORY;
   } catch (const std::exception& e) {
-    g_last_error = e.what();
+    set_last_error(e.what());
     return TPL_ERR_INVALID_ARGUMENT;
   }
-}
-
-// ------------------------------------------------------------ layout
-struct SchedParams {
-  int short_row_max = -1;           // rows longer than this are sliced; -1 = auto
-  int max_g2 = 1024;                // element-wise workgroups (== #norm partials)
-  int64_t long_from = -1;           // >= 0: rows [long_from, n) are long, the rest short
-  bool compress_values = true;      // int8 values when all values are small integers
-  bool compress_cols = true;        // uint16 column offsets when the spans allow
-  int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
-};
-
-// Column slices of the long rows (auto rule): the fewest (1, 2, 4, 8) whose share of
-// the gathered vector fits in an eighth of an XCD's 4 MiB L2 (measured at 500k arcs with
-// the arrival-counter hand-off: 8 slices 11.91 ms per k = 500 solve, 4 slices 12.23, 2
-// slices 13.61; at 50k: 1 slice 7.1 ms, 2 slices 9.1) — slice s runs on the XCDs
-// b % 8 == s (mod slices), so each L2 caches only its slice's columns — and, when a
-// (row, slice) piece would exceed one bin, more slices until every piece fits.
-static int auto_slices(int64_t n_cols) {
-  int s = 1;
-  while (s < kSlices && (double)n_cols * 8.0 / s > 0.5 * 1024.0 * 1024.0) s *= 2;
-  return s;
-}
-
-// Host copy of the SpMV layout (tpl_device.h).
-struct Layout {
-  std::vector<int32_t> srows;       // short rows, ascending
-  std::vector<int32_t> s_col;       // sliced ELL entries (col = -1: padding)
-  std::vector<double> s_val;
-  std::vector<int32_t> c_base, c_width;
-  int32_t s_width = 0;              // uniform chunk width (0: per-chunk)
-  int32_t s_identity = 0;
-  std::vector<int32_t> lrows;       // long rows, ascending
-  std::vector<int32_t> b_col;       // long-row bins: n_bins x bin_cap entries
-  std::vector<double> b_val;
-  bool val_i8 = false;              // every value a small integer: stored as int8
-  std::vector<int8_t> s_val8, b_val8;
-  bool s_col16 = false, b_col16 = false;  // uint16 column offsets from a per-chunk/bin base
-  std::vector<uint16_t> s_col16v, b_col16v;
-  std::vector<int32_t> s_cbase, b_cbase;
-  int32_t nslices = 1;              // column slices of the long rows
-  std::vector<BinSeg> b_seg;        // n_bins x kTPB table slots
-  std::vector<int32_t> b_hdr;       // per bin: pieces | long pieces << 16
-  int32_t bin_cap = kBinMin;
-  int32_t M = 0;                    // bins per slice
-  int G2 = 1;
-  int64_t E = 512;
-  int32_t s_win = 0, s_win_max = 0;  // short-chunk column window (tpl_device.h)
-};
-
-// Auto rule: T = clamp(2 * median row length, 4, kShortRowMax). A sliced-ELL chunk
-// costs as much as its widest row, so the few rows far above the typical length
-// (e.g. the short node rows of a KKT matrix) go to the sliced long-row path instead
-// of widening a chunk.
-static int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int requested) {
-  if (requested > 0) return requested;
-  if (n == 0) return kShortRowMax;
-  std::vector<int32_t> hist(kShortRowMax + 2, 0);
-  for (int64_t i = 0; i < n; ++i) hist[std::min<int32_t>(rp[i + 1] - rp[i], kShortRowMax + 1)]++;
-  int64_t seen = 0;
-  int32_t median = kShortRowMax + 1;
-  for (int32_t l = 0; l <= kShortRowMax + 1; ++l) {
-    seen += hist[l];
-    if (2 * seen >= n) {  // lower median
-      median = l;
-      break;
-    }
-  }
-  return std::max<int32_t>(4, std::min<int32_t>(kShortRowMax, 2 * median));
-}
-
-// Column index as stored on the device: the identity on one GPU; with the rows
-// partitioned over ranks, global column c (owned by rank r, rows [starts[r],
-// starts[r+1])) lives at r * ld + (c - starts[r]) of the all-gathered vector.
-struct ColMap {
-  const std::vector<int64_t>* starts = nullptr;  // row partition (nullptr: see table)
-  int64_t ld = 0;
-  int32_t operator()(int32_t c) const {
-    if (!starts) return c;
-    const auto it = std::upper_bound(starts->begin(), starts->end(), (int64_t)c);
-    const int64_t r = (it - starts->begin()) - 1;
-    return (int32_t)(r * ld + (c - (*starts)[r]));
-  }
-};
-
-// n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds
-// are taken on global column indices, so a partition of one rank reproduces the
-// single-GPU layout exactly).
-static Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
-                           const std::vector<int32_t>& col, const std::vector<double>& val,
-                           const SchedParams& sp, const ColMap& cmap) {
-  Layout L;
-  const int32_t T = short_row_threshold(n, rp, sp.short_row_max);
-  for (int64_t i = 0; i < n; ++i) {
-    if (sp.long_from >= 0 ? i >= sp.long_from : rp[i + 1] - rp[i] > T) L.lrows.push_back((int32_t)i);
-    else L.srows.push_back((int32_t)i);
-  }
-  const int64_t ns = (int64_t)L.srows.size();
-  L.s_identity = 1;
-  for (int64_t p = 0; p < ns; ++p)
-    if (L.srows[p] != p) {
-      L.s_identity = 0;
-      break;
-    }
-  const int64_t nchunks = (ns + kChunkRows - 1) / kChunkRows;
-  L.c_base.resize(nchunks);
-  L.c_width.resize(nchunks);
-  int64_t total = 0;
-  for (int64_t c = 0; c < nchunks; ++c) {
-    int32_t w = 0;
-    for (int64_t p = c * kChunkRows; p < std::min(ns, (c + 1) * kChunkRows); ++p)
-      w = std::max<int32_t>(w, rp[L.srows[p] + 1] - rp[L.srows[p]]);
-    L.c_base[c] = (int32_t)total;
-    L.c_width[c] = w;
-    total += (int64_t)w * kChunkRows;
-  }
-  if (total >= INT32_MAX) fail(TPL_ERR_UNSUPPORTED, "sliced-ELL storage exceeds 2^31 entries");
-  L.s_col.assign(std::max<int64_t>(total, 1), -1);
-  L.s_val.assign(std::max<int64_t>(total, 1), 0.0);
-  for (int64_t c = 0; c < nchunks; ++c)
-    for (int64_t p = c * kChunkRows; p < std::min(ns, (c + 1) * kChunkRows); ++p) {
-      const int32_t r = L.srows[p];
-      for (int32_t k = 0; k < rp[r + 1] - rp[r]; ++k) {
-        const int64_t e = L.c_base[c] + (int64_t)k * kChunkRows + (p - c * kChunkRows);
-        L.s_col[e] = cmap(col[rp[r] + k]);
-        L.s_val[e] = val[rp[r] + k];
-      }
-    }
-  L.s_width = 0;
-  if (nchunks > 0) {
-    bool uni = true;
-    for (int64_t c = 0; c < nchunks; ++c) uni = uni && L.c_width[c] == L.c_width[0];
-    if (uni && L.c_width[0] > 0) L.s_width = L.c_width[0];
-  }
-  const size_t nl = L.lrows.size();
-  // Long rows: piece (r, s) = entries of long row r with columns in slice s (columns
-  // [n_glob s / S, n_glob (s+1) / S)); the pieces of slice s, r ascending, are packed
-  // whole into bins (first fit in order).
-  const size_t nlb = nl;
-  int S = sp.slices > 0 ? sp.slices : auto_slices(n_glob);
-  std::vector<int32_t> poff;
-  int32_t widest = 0;
-  auto cut = [&](int ns) {
-    poff.assign(nlb * (ns + 1), 0);
-    widest = 0;
-    for (size_t r = 0; r < nlb; ++r) {
-      const int32_t row = L.lrows[r];
-      int32_t q = rp[row];
-      for (int s = 0; s <= ns; ++s) {
-        const int64_t bound = n_glob * s / ns;
-        while (q < rp[row + 1] && col[q] < bound) ++q;
-        poff[r * (ns + 1) + s] = (s == ns) ? rp[row + 1] : q;
-        if (s > 0) widest = std::max(widest, poff[r * (ns + 1) + s] - poff[r * (ns + 1) + s - 1]);
-      }
-    }
-  };
-  cut(S);
-  while (widest > kBinMax && sp.slices <= 0 && S < kSlices) cut(S *= 2);
-  if (widest > kBinMax)
-    fail(TPL_ERR_UNSUPPORTED, "a long row has " + std::to_string(widest) +
-                                  " nonzeros in one of its " + std::to_string(S) +
-                                  " column slices (limit " + std::to_string(kBinMax) + ")");
-  L.nslices = S;
-  L.bin_cap = std::max<int32_t>(kBinMin, ((widest + kTPB - 1) / kTPB) * kTPB);
-  L.bin_cap = ((L.bin_cap + kBinMin - 1) / kBinMin) * kBinMin;  // whole load batches
-  std::vector<std::vector<std::vector<std::pair<int32_t, int32_t>>>> bins(S); // (r, fill-at-start)
-  std::vector<std::vector<int32_t>> fill(S);
-  for (int s = 0; s < S && nlb > 0; ++s) {
-    for (size_t r = 0; r < nlb; ++r) {
-      const int32_t cnt = poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
-      if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
-          (int)bins[s].back().size() == kBinSegs) {
-        bins[s].emplace_back();
-        fill[s].push_back(0);
-      }
-      bins[s].back().emplace_back((int32_t)r, fill[s].back());
-      fill[s].back() += cnt;
-    }
-  }
-  L.M = 0;
-  for (int s = 0; s < S; ++s) L.M = std::max<int32_t>(L.M, (int32_t)bins[s].size());
-  const size_t nbins = (size_t)S * L.M;
-  L.b_col.assign(std::max<size_t>(nbins * L.bin_cap, 1), -1);
-  L.b_val.assign(std::max<size_t>(nbins * L.bin_cap, 1), 0.0);
-  L.b_seg.assign(std::max<size_t>(nbins * kTPB, 1), BinSeg{0, -1, -1, 0});
-  L.b_hdr.assign(std::max<size_t>(nbins, 1), 0);
-  for (int s = 0; s < S; ++s)
-    for (int32_t m = 0; m < L.M; ++m) {
-      const size_t bin = (size_t)m * S + s;
-      int32_t f = 0;
-      if (m < (int32_t)bins[s].size()) {
-        // the pieces longer than kBigPiece first (summed a wave each), then the rest;
-        // entries are laid out in that table order
-        auto pieces = bins[s][m];
-        auto len = [&](int32_t r) {
-          return poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
-        };
-        std::stable_partition(pieces.begin(), pieces.end(),
-                              [&](const std::pair<int32_t, int32_t>& p) { return len(p.first) > kBigPiece; });
-        int32_t nbig = 0, at = 0;
-        for (auto& p : pieces) {
-          nbig += len(p.first) > kBigPiece;
-          p.second = at;
-          at += len(p.first);
-        }
-        for (size_t j = 0; j < pieces.size(); ++j) {
-          const int32_t r = pieces[j].first, start = pieces[j].second;
-          const int32_t q0 = poff[r * (S + 1) + s], q1 = poff[r * (S + 1) + s + 1];
-          L.b_seg[bin * kTPB + j] = BinSeg{start, r, L.lrows[r], 0};
-          for (int32_t q = q0; q < q1; ++q) {
-            L.b_col[bin * L.bin_cap + start + (q - q0)] = cmap(col[q]);
-            L.b_val[bin * L.bin_cap + start + (q - q0)] = val[q];
-          }
-        }
-        f = fill[s][m];
-        for (size_t j = pieces.size(); j < (size_t)kTPB; ++j)
-          L.b_seg[bin * kTPB + j] = BinSeg{f, -1, -1, 0};
-        L.b_hdr[bin] = (int32_t)pieces.size() | nbig << 16;
-      }
-    }
-  // Value compression: when every stored value (padding included) is an integer in
-  // [-128, 127] other than -0.0, keep int8 values; the device converts them back to
-  // double exactly, so every product and sum keeps its bits (the KKT values are +-1).
-  auto small_int = [](double v) {
-    return v >= -128.0 && v <= 127.0 && v == (double)(int8_t)v && !(v == 0.0 && std::signbit(v));
-  };
-  L.val_i8 = sp.compress_values;
-  for (double v : L.s_val) L.val_i8 = L.val_i8 && small_int(v);
-  for (double v : L.b_val) L.val_i8 = L.val_i8 && small_int(v);
-  if (L.val_i8) {
-    L.s_val8.assign(L.s_val.begin(), L.s_val.end());
-    L.b_val8.assign(L.b_val.begin(), L.b_val.end());
-    std::vector<double>().swap(L.s_val);
-    std::vector<double>().swap(L.b_val);
-  }
-  // Column compression: uint16 offsets from each chunk's / bin's smallest column when
-  // every chunk / bin spans fewer than 65535 columns (0xFFFF marks padding).
-  auto compress_cols = [&](const std::vector<int32_t>& cols, int64_t groups, int64_t per,
-                           std::vector<uint16_t>& out16, std::vector<int32_t>& base) {
-    if (!sp.compress_cols || groups == 0) return false;
-    base.assign(groups, 0);
-    for (int64_t g = 0; g < groups; ++g) {
-      int32_t lo = INT32_MAX, hi = -1;
-      for (int64_t e = g * per; e < (g + 1) * per && e < (int64_t)cols.size(); ++e)
-        if (cols[e] >= 0) {
-          lo = std::min(lo, cols[e]);
-          hi = std::max(hi, cols[e]);
-        }
-      if (hi < 0) lo = hi = 0;
-      if (hi - lo >= 0xFFFF) return false;
-      base[g] = lo;
-    }
-    out16.resize(cols.size());
-    for (size_t e = 0; e < cols.size(); ++e)
-      out16[e] = cols[e] < 0 ? 0xFFFF : (uint16_t)(cols[e] - base[e / per]);
-    return true;
-  };
-  // chunks have a uniform stride only when the widths are uniform (else per-chunk bases)
-  if (L.s_width > 0)
-    L.s_col16 = compress_cols(L.s_col, nchunks, (int64_t)L.s_width * kChunkRows, L.s_col16v, L.s_cbase);
-  L.b_col16 = compress_cols(L.b_col, (int64_t)L.nslices * L.M, L.bin_cap, L.b_col16v, L.b_cbase);
-  // Column window of the short chunks: every chunk's columns within kWinMax of its base
-  // (uint16 columns, uniform width 1..4) -> staged in LDS (TPL_NO_WIN=1: off, experiments).
-  if (L.s_col16 && L.s_width >= 1 && L.s_width <= 4 && !(std::getenv("TPL_NO_WIN") &&
-                                                          std::getenv("TPL_NO_WIN")[0] == '1')) {
-    const int64_t per = (int64_t)L.s_width * kChunkRows;
-    int32_t win = 0, hi = 0;
-    for (int64_t c = 0; c < nchunks; ++c)
-      for (int64_t e = c * per; e < (c + 1) * per; ++e)
-        if (L.s_col[e] >= 0) {
-          win = std::max<int32_t>(win, L.s_col[e] - L.s_cbase[c] + 1);
-          hi = std::max<int32_t>(hi, L.s_col[e]);
-        }
-    if (win > 0 && win <= kWinMax) {
-      L.s_win = win;
-      L.s_win_max = hi;
-    }
-  }
-  if (L.s_col16) std::vector<int32_t>().swap(L.s_col);
-  if (L.b_col16) std::vector<int32_t>().swap(L.b_col);
-  const int64_t g2 = (n + kElemRows - 1) / kElemRows;
-  L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
-  const int64_t per = (n + L.G2 - 1) / L.G2;
-  L.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
-  return L;
 }
 
 } // namespace tpl
@@ -1072,7 +768,6 @@ void balanced_cuts(const std::vector<double>& prefix, int nranks, int64_t* start
 // =========================================================== C ABI
 extern "C" {
 
-const char* tpl_last_error(void) { return g_last_error.c_str(); }
 const char* tpl_version(void) { return "tpl_amd 0.1.0 gfx950"; }
 
 int tpl_device_count(void) {
