@@ -319,7 +319,10 @@ def main():
                                             al.ctypes.data_as(PD), be.ctypes.data_as(PD),
                                             ctypes.byref(st), ctypes.byref(bn), None,
                                             _lib.TPL_MEM_DEVICE, reorth, None, None))
-        tm = {r: time_solves(lambda: one_pass(r), 2, torch.cuda.synchronize) for r in (0, 1)}
+        tm, second = {}, {}
+        for r in (0, 1, 2):
+            tm[r] = time_solves(lambda: one_pass(r), 2, torch.cuda.synchronize)
+            second[r] = op.reorth_second_passes()
         s1 = int(st.value)
         rb = sum(2.0 * (16.0 * n * j + 24.0 * n) for j in range(1, s1))
         rate = rb / max(tm[1] - tm[0], 1e-9) / 1e9
@@ -329,6 +332,15 @@ def main():
             "plain_one_pass_ms": round(1000 * tm[0], 3),
             "reorth_bytes": rb, "reorth_GBs": round(rate, 1),
             "reorth_frac_of_hbm": round(rate / HBM_PEAK_GBS, 4)}
+        # the selective (Kahan–Parlett) variant: the second pass only where needed; its
+        # bytes: one pass per step plus a second pass on `second_passes` steps
+        rb2 = sum(16.0 * n * j + 24.0 * n for j in range(1, s1)) * (1.0 + second[2] / max(s1 - 1, 1))
+        rate2 = rb2 / max(tm[2] - tm[0], 1e-9) / 1e9
+        out["one_pass_reorth_selective"] = {
+            "config": f"lanczos_standard k={args.k} + selective CGS (Kahan-Parlett twice-is-enough)",
+            "ms_per_solve": round(1000 * tm[2], 2), "iterations_per_s": round(s1 / tm[2], 1),
+            "second_passes": second[2], "steps": s1,
+            "reorth_GBs": round(rate2, 1), "reorth_frac_of_hbm": round(rate2 / HBM_PEAK_GBS, 4)}
     if world == 1 and not partitioned and args.other_configs:
         # BASELINE configs[0] and [1] on the same GPU (parity-test sizes; reported, not `value`)
         others = {}

@@ -161,8 +161,11 @@ typedef int (*tpl_step_cb)(size_t k, const double* v_k_device, int64_t n,
 /* algorithms::lanczos::lanczos_standard (src/algorithms/lanczos.rs:55-156).
  * alphas: capacity k; betas: capacity k (k-1 used); v_out: n x k capacity or NULL.
  * On return *steps = steps_taken, *b_norm = ||b||, alphas[0..steps), betas[0..steps-1),
- * v_out columns [0, steps) filled. reorth != 0 enables full re-orthogonalisation
- * (CGS2 against the stored V_k; an extension with no reference counterpart).   */
+ * v_out columns [0, steps) filled. reorth enables full re-orthogonalisation against
+ * the stored V_k (an extension with no reference counterpart): 1 = CGS2 (classical
+ * Gram-Schmidt, two passes every step), 2 = selective (Kahan–Parlett "twice is
+ * enough": the second pass only when the first removed more than half of ||r||^2;
+ * tpl_op_reorth_second_passes reports how many ran), 0 = none.                  */
 tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                                 double* alphas, double* betas, size_t* steps,
                                 double* b_norm, double* v_out, int mem, int reorth,
@@ -228,6 +231,9 @@ tpl_status tpl_op_set_schedule(tpl_op_t op, int32_t short_row_max, int32_t max_g
 tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices);
 tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices);
 
+/* Second Gram-Schmidt passes of the last re-orthogonalised tpl_lanczos_standard call
+ * (steps - 1 for CGS2; the count the selective mode actually ran).                */
+tpl_status tpl_op_reorth_second_passes(tpl_op_t op, int64_t* count);
 /* Device memory the operator holds now, in bytes: its layout (matrix in the engine's
  * format), the ten n-vectors of the recurrence, the solver state and — once a one-pass
  * solve (tpl_lanczos / tpl_lanczos_standard) has run — the basis V_k (8 n k bytes).

@@ -207,9 +207,15 @@ static double nrm2_faithful(int64_t n, const double* x) {
  * r[i], acc) over i = bE + t + 256q; tree256), then r[i] = r[i] - s_i with s_i = 0;
  * s_i = fma(V[c][i], h[c], s_i), c ascending. (Extension: the reference has no
  * re-orthogonalisation; pinned only against this restatement and orthonormality.) */
+static double nrm2_canon(const osched* S, int64_t n, const double* x, double* P);
+/* mode 1: CGS2 (two passes). mode 2: selective (Kahan–Parlett, k_reorth_decide): the
+ * second pass runs only if ||r'||^2 < ||r||^2 / 2 after the first, both squared norms in
+ * the canonical norm order. */
 static void reorth_canon(const osched* S, int64_t n, const double* V, int cols, double* r,
-                         double* P, double* h) {
+                         double* P, double* h, int mode) {
+  const double n0 = mode == 2 ? nrm2_canon(S, n, r, P) : 0.0;
   for (int pass = 0; pass < 2; ++pass) {
+    if (mode == 2 && pass == 1 && nrm2_canon(S, n, r, P) >= 0.5 * n0) break;
     /* P[c * G2 + b]: the (column, workgroup) trees; workgroups are independent */
 #pragma omp parallel for schedule(static)
     for (int b = 0; b < S->G2; ++b) {
@@ -273,7 +279,7 @@ static int pass_one_impl(const ocsr* A, const osched* S, const double* b, size_t
     if (it + 1 == k) break; /* beta_k is never used */
     #pragma omp parallel for schedule(static)
     for (int64_t i = 0; i < n; ++i) w[i] = w[i] - alpha * vc[i];     /* :196-198 */
-    if (reorth) reorth_canon(S, n, V, (int)(it + 1), w, P, h);        /* extension */
+    if (reorth) reorth_canon(S, n, V, (int)(it + 1), w, P, h, reorth); /* extension */
     const double beta = sqrt(S ? nrm2_canon(S, n, w, P) : nrm2_faithful(n, w)); /* :202 */
     if (beta <= TOL) break;                                           /* :206-208 */
     betas[nb++] = beta;
@@ -298,6 +304,12 @@ int oracle_pass_one_reorth(const ocsr* A, const osched* S, const double* b, size
                            double* alphas, double* betas, size_t* steps, double* bnorm_out,
                            double* V) {
   return pass_one_impl(A, S, b, k, alphas, betas, steps, bnorm_out, V, 1);
+}
+/* ... with the selective (Kahan–Parlett) variant. */
+int oracle_pass_one_reorth_selective(const ocsr* A, const osched* S, const double* b, size_t k,
+                                     double* alphas, double* betas, size_t* steps,
+                                     double* bnorm_out, double* V) {
+  return pass_one_impl(A, S, b, k, alphas, betas, steps, bnorm_out, V, 2);
 }
 
 /* Pass two; y already scaled by ||b||. V (n x steps) may be NULL. */

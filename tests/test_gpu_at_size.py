@@ -129,6 +129,31 @@ def test_config3_reorth_500k_bitwise_k150(op500k, kkt500k):
 
 
 @pytest.mark.timeout(600)
+def test_config3_selective_reorth_500k(op500k, kkt500k):
+    """configs[3] with the selective (Kahan–Parlett) variant: k = 500 properties at size
+    (orthonormality, Lanczos relation, determinism) and k = 150 bitwise vs the oracle."""
+    a = kkt500k.a
+    b = harness_b(a)
+    bd = torch.from_numpy(b).cuda()
+    out = alg.lanczos_standard(op500k, bd, 500, reorthogonalize="selective")
+    d = out.decomposition
+    assert d.steps_taken == 500
+    V = basis_rows(out)
+    loss = float(torch.linalg.norm(torch.eye(500, dtype=torch.float64, device="cuda") - V @ V.T))
+    assert loss < 1e-12, loss
+    assert relation_residual(op500k, V, d.alphas, d.betas) < 1e-10
+    out2 = alg.lanczos_standard(op500k, bd, 500, reorthogonalize="selective")
+    assert np.array_equal(out2.decomposition.betas, d.betas)
+    k = 150
+    out = alg.lanczos_standard(op500k, bd, k, reorthogonalize="selective")
+    al, be, st, bn, Vo = canon(op500k, a).pass_one(b, k, reorth="selective")
+    d = out.decomposition
+    assert d.steps_taken == st == k and d.b_norm == bn
+    assert np.array_equal(d.alphas, al) and np.array_equal(d.betas, be)
+    assert torch.equal(basis_rows(out), torch.from_numpy(np.ascontiguousarray(Vo.T)).cuda())
+
+
+@pytest.mark.timeout(600)
 def test_config3_plain_one_pass_500k_k500_bitwise(op500k, kkt500k):
     """solvers::lanczos (standard pass + device GEMV x = ||b|| V_k y') at 500k, k = 500,
     f = inv: x bit for bit against the canonical oracle; V_k against pass two's

@@ -433,6 +433,32 @@ def test_reorthogonalization_extension(op5k, kkt5k):
     assert np.array_equal(np.asarray(V), Vo)
 
 
+@pytest.mark.parametrize("which", ["kkt5k", "skewed"])
+def test_selective_reorthogonalization_bitwise(which, op5k, kkt5k, skewed):
+    """Selective (Kahan–Parlett) re-orthogonalisation: the second Gram-Schmidt pass only
+    where the first removed more than half of ||r||^2 — the device's decisions and every
+    value bit for bit against the oracle's restatement; orthonormal like CGS2."""
+    a = kkt5k.a if which == "kkt5k" else skewed
+    op = op5k if which == "kkt5k" else HipCsrOp(a)
+    b = std_rng_vector(a.shape[0])
+    k = 150
+    re = alg.lanczos_standard(op, b, k, reorthogonalize="selective")
+    second = op.reorth_second_passes()
+    s = re.decomposition.steps_taken
+    V = np.asarray(re.v_k)
+    assert np.linalg.norm(np.eye(s) - V.T @ V) < 1e-12
+    assert 0 <= second < s
+    al, be, st, bn, Vo = canon(op, a).pass_one(b, k, reorth="selective")
+    assert st == s and bn == re.decomposition.b_norm
+    assert np.array_equal(re.decomposition.alphas, al)
+    assert np.array_equal(re.decomposition.betas, be)
+    assert np.array_equal(V, Vo)
+    cg = alg.lanczos_standard(op, b, k, reorthogonalize=True)
+    assert op.reorth_second_passes() == cg.decomposition.steps_taken - 1
+    with pytest.raises(ValueError):
+        alg.lanczos_standard(op, b, k, reorthogonalize="mgs")
+
+
 def test_device_pointer_path(op5k, kkt5k):
     torch = pytest.importorskip("torch")
     b = harness_b(kkt5k.a)

@@ -48,6 +48,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
     S.flags[0] = 0;
     S.flags[1] = 0;
     S.flags[2] = 0;
+    S.flags[3] = 0;
   }
   const int rb = elem_block(A, blockIdx.x);
   if (rb < 0) return;
@@ -448,11 +449,14 @@ constexpr int kReorthCols = 16; // columns per workgroup in the h = V^T r kernel
 // t: acc = fma(V[c][i], r[i], acc) over i = bE + t + 256q, q ascending). Every column's
 // load is issued unconditionally (columns past cols re-read column 16g, unused) so the
 // 17 loads of an iteration are all in flight; the 16 trees share one barrier.
+// skip (selective variant): the second pass is not needed (k_reorth_decide).
 __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
                                                      const double* __restrict__ V,
                                                      const double* __restrict__ r,
-                                                     double* __restrict__ P, int G, int64_t E) {
+                                                     double* __restrict__ P, int G, int64_t E,
+                                                     const int* __restrict__ skip) {
   __shared__ double red[kReorthCols * 4];
+  if (skip && *skip) return;
   const int c0 = blockIdx.y * kReorthCols;
   const int nc = cols - c0 < kReorthCols ? cols - c0 : kReorthCols;
   const int64_t beg = (int64_t)blockIdx.x * E;
@@ -484,8 +488,10 @@ __global__ __launch_bounds__(kTPB) void k_reorth_dot(int64_t n, int cols,
 
 // h[c] = sum of the G partials of column c (one workgroup per column).
 __global__ __launch_bounds__(kTPB) void k_reorth_reduce(const double* __restrict__ P, int G,
-                                                        double* __restrict__ h) {
+                                                        double* __restrict__ h,
+                                                        const int* __restrict__ skip) {
   __shared__ double red[4];
+  if (skip && *skip) return;
   PartialRegs<8> pr;
   const double* Pc = P + (int64_t)blockIdx.x * G;
   load_partials(Pc, G, pr);
@@ -504,8 +510,10 @@ __global__ __launch_bounds__(kTPB) void k_reorth_update(int64_t n, int cols,
                                                         const double* __restrict__ V,
                                                         double* __restrict__ r,
                                                         const double* __restrict__ h,
-                                                        double* __restrict__ Pnorm, int64_t E) {
+                                                        double* __restrict__ Pnorm, int64_t E,
+                                                        const int* __restrict__ skip) {
   __shared__ double red[4];
+  if (skip && *skip) return;
   const int64_t beg = (int64_t)blockIdx.x * E;
   const int64_t end = beg + E < n ? beg + E : n;
   double acc = 0.0;
@@ -546,6 +554,29 @@ __global__ __launch_bounds__(kTPB) void k_reorth_update(int64_t n, int cols,
   if (Pnorm) {
     const double p = block_sum(acc, red);
     if (threadIdx.x == 0) Pnorm[blockIdx.x] = p;
+  }
+}
+
+// Selective re-orthogonalisation (Kahan–Parlett "twice is enough"): after the first
+// projection r' = r - V h, the second one is needed only when it removed more than half
+// of r's squared norm. n0 = ||r||^2 (the partials k_p1_axpy left in S.Pb), n1 = ||r'||^2
+// (Pb1, written by the first update), both reduced in the canonical norm order; if
+// n1 >= n0 / 2 the second pass is skipped and r' is the result — its partials become the
+// ones k_p1_spmv reduces for beta — else S.flags[3] counts a second pass. One workgroup.
+__global__ __launch_bounds__(kTPB) void k_reorth_decide(DevState S, const double* __restrict__ Pb1,
+                                                        int G2, int* __restrict__ skip) {
+  __shared__ double red[4];
+  PartialRegs<4> p0, p1;  // G2 <= 1024
+  load_partials(S.Pb, G2, p0);
+  load_partials(Pb1, G2, p1);
+  const double n0 = finish_partials(S.Pb, G2, p0, red);
+  const double n1 = finish_partials(Pb1, G2, p1, red);
+  const bool sk = n1 >= 0.5 * n0;
+  if (sk)
+    for (int i = threadIdx.x; i < G2; i += kTPB) S.Pb[i] = Pb1[i];
+  if (threadIdx.x == 0) {
+    *skip = sk ? 1 : 0;
+    if (!sk) S.flags[3] = S.flags[3] + 1;
   }
 }
 
@@ -674,18 +705,24 @@ hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, 
   return hipGetLastError();
 }
 hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
-                      int64_t E, hipStream_t s) {
+                      int64_t E, const int* skip, hipStream_t s) {
   dim3 grid(G, (cols + kReorthCols - 1) / kReorthCols);
-  hipLaunchKernelGGL(k_reorth_dot, grid, dim3(kTPB), 0, s, n, cols, V, r, P, G, E);
+  hipLaunchKernelGGL(k_reorth_dot, grid, dim3(kTPB), 0, s, n, cols, V, r, P, G, E, skip);
   return hipGetLastError();
 }
-hipError_t reorth_reduce(int cols, const double* P, int G, double* h, hipStream_t s) {
-  hipLaunchKernelGGL(k_reorth_reduce, dim3(cols), dim3(kTPB), 0, s, P, G, h);
+hipError_t reorth_reduce(int cols, const double* P, int G, double* h, const int* skip,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_reorth_reduce, dim3(cols), dim3(kTPB), 0, s, P, G, h, skip);
   return hipGetLastError();
 }
 hipError_t reorth_update(int64_t n, int cols, const double* V, double* r, const double* h,
-                         double* Pnorm, int G, int64_t E, hipStream_t s) {
-  hipLaunchKernelGGL(k_reorth_update, dim3(G), dim3(kTPB), 0, s, n, cols, V, r, h, Pnorm, E);
+                         double* Pnorm, int G, int64_t E, const int* skip, hipStream_t s) {
+  hipLaunchKernelGGL(k_reorth_update, dim3(G), dim3(kTPB), 0, s, n, cols, V, r, h, Pnorm, E,
+                     skip);
+  return hipGetLastError();
+}
+hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip, hipStream_t s) {
+  hipLaunchKernelGGL(k_reorth_decide, dim3(1), dim3(kTPB), 0, s, S, Pb1, G2, skip);
   return hipGetLastError();
 }
 

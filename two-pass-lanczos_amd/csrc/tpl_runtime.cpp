@@ -51,11 +51,12 @@ hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, i
                        const double* v_cur, const double* v_prev, double* v_next, double* x,
                        double* Vcol, int j, int nflush, hipStream_t s);
 hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hipStream_t s);
+hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip, hipStream_t s);
 hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
-                      int64_t E, hipStream_t s);
-hipError_t reorth_reduce(int cols, const double* P, int G, double* h, hipStream_t s);
+                      int64_t E, const int* skip, hipStream_t s);
+hipError_t reorth_reduce(int cols, const double* P, int G, double* h, const int* skip, hipStream_t s);
 hipError_t reorth_update(int64_t n, int cols, const double* V, double* r, const double* h,
-                         double* Pnorm, int G, int64_t E, hipStream_t s);
+                         double* Pnorm, int G, int64_t E, const int* skip, hipStream_t s);
 } // namespace launch
 
 #define HIPCHK(expr)                                                                        \
@@ -183,6 +184,7 @@ struct tpl_op_s {
   bool timing = false;
   int device_ftk = 2;               // built-in inv on the device (one graph): 0 off, 1 on, 2 auto
   bool last_one_graph = false;      // the last tpl_lanczos_two_pass ran as one device graph
+  int64_t reorth_second = 0;        // second Gram-Schmidt passes of the last reorth solve
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
 };
@@ -341,8 +343,9 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->kcap = kc;
   }
   if (reorth && !op->d_Pr) {
-    // [cols x G partials][cols coefficients]
-    dev_alloc(op, &op->d_Pr, ((size_t)op->lay.G2 + 1) * op->kcap * sizeof(double));
+    // [cols x G partials][cols coefficients][G norm partials after the first pass][skip flag]
+    dev_alloc(op, &op->d_Pr,
+              (((size_t)op->lay.G2 + 1) * op->kcap + (size_t)op->lay.G2 + 1) * sizeof(double));
   }
 }
 
@@ -414,25 +417,33 @@ void dist_group(tpl_op_s* op, bool begin) {
 // This rank's total of a partial array, in the single-GPU canonical order, into
 // its slot of the all-gathered totals.
 void dist_total(tpl_op_s* op, const double* P, int N, double* slot) {
-  HIPCHK(launch::reorth_reduce(1, P, N, slot, op->stream));
+  HIPCHK(launch::reorth_reduce(1, P, N, slot, nullptr, op->stream));
 }
 
-// ---- reorthogonalisation (extension, not in the reference): classical Gram-Schmidt,
-// applied twice, of r_{j+1} against the stored columns V[:, 0..j) before beta_j.
-void enqueue_reorth(tpl_op_s* op, int j) {
+// ---- reorthogonalisation (extension, not in the reference): classical Gram-Schmidt of
+// r_{j+1} against the stored columns V[:, 0..j) before beta_j. mode 1 (CGS2): two
+// passes, always. mode 2 (selective, Kahan–Parlett "twice is enough"): the second pass
+// runs only when the first removed more than half of ||r||^2 (k_reorth_decide; its
+// kernels see the device flag and return at once otherwise).
+void enqueue_reorth(tpl_op_s* op, int j, int mode) {
   if (op->dist) fail(TPL_ERR_UNSUPPORTED, "re-orthogonalisation of a partitioned operator");
   const int cols = j; // v_1 .. v_j are stored in V[:, 0..j)
   const int G2 = op->lay.G2;
   const int64_t E = op->lay.E;
   double* P = op->d_Pr;                             // cols x G2 partials
   double* h = op->d_Pr + (size_t)G2 * op->kcap;    // cols coefficients
+  double* Pb1 = h + op->kcap;                      // ||r'||^2 partials (selective)
+  int* skip = reinterpret_cast<int*>(Pb1 + G2);
   double* r = op->R[(j + 1) % 3];
   for (int pass = 0; pass < 2; ++pass) {
-    HIPCHK(launch::reorth_dot(op->n, cols, op->d_V, r, P, G2, E, op->stream));
-    HIPCHK(launch::reorth_reduce(cols, P, G2, h, op->stream));
-    // the second update also rewrites the ||r||^2 partials that k_p1_spmv(j+1) reduces
-    HIPCHK(launch::reorth_update(op->n, cols, op->d_V, r, h, pass == 1 ? op->S.Pb : nullptr,
-                                 G2, E, op->stream));
+    const int* sk = (mode == 2 && pass == 1) ? skip : nullptr;
+    HIPCHK(launch::reorth_dot(op->n, cols, op->d_V, r, P, G2, E, sk, op->stream));
+    HIPCHK(launch::reorth_reduce(cols, P, G2, h, sk, op->stream));
+    // the last update rewrites the ||r||^2 partials that k_p1_spmv(j+1) reduces; in the
+    // selective mode the first one writes its own partials for the decision
+    double* pn = pass == 1 ? op->S.Pb : (mode == 2 ? Pb1 : nullptr);
+    HIPCHK(launch::reorth_update(op->n, cols, op->d_V, r, h, pn, G2, E, sk, op->stream));
+    if (mode == 2 && pass == 0) HIPCHK(launch::reorth_decide(op->S, Pb1, G2, skip, op->stream));
   }
 }
 
@@ -494,12 +505,12 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
   }
 }
 
-void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, bool reorth) {
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth) {
   enqueue_p1_prologue(op);
   for (int j = 1; j <= (int)k; ++j) {
     double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
     enqueue_p1_step(op, j, (int)k, Vcol);
-    if (reorth && j < (int)k) enqueue_reorth(op, j);
+    if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
   }
 }
 
@@ -654,12 +665,12 @@ void run_two_pass_dev(tpl_op_s* op, size_t k) {
   op->p2_launches = (int64_t)k - 1;
 }
 
-void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV, bool reorth) {
+void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV, int reorth) {
   ensure_state(op, k, reorth);
   if (storeV) ensure_basis(op, k);
   upload_vec(op, op->b, b, mem);
   if (reorth) {
-    enqueue_pass1(op, k, true, true); // eager: reorth launch counts vary with j
+    enqueue_pass1(op, k, true, reorth); // eager: reorth launch counts vary with j
   } else {
     if (op->timing) HIPCHK(hipEventRecord(op->tev[0], op->stream));
     run_graph(op, storeV ? kGStandard : kGPass1, k, [&] { enqueue_pass1(op, k, storeV, false); });
@@ -940,7 +951,8 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
     check_k(k);
     HostDecomp d;
     if (!cb) {
-      run_pass_one(op, b, k, mem, true, reorth != 0);
+      if (reorth < 0 || reorth > 2) fail(TPL_ERR_INVALID_ARGUMENT, "reorth must be 0, 1 or 2");
+      run_pass_one(op, b, k, mem, true, reorth);
       d = fetch_decomp(op, k);
     } else {
       // src/algorithms/lanczos.rs:86-128 with the host callback after every step, polled
@@ -961,7 +973,7 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
         const int j1 = std::min<int>((int)k, j0 + batch - 1);
         for (int j = j0; j <= j1; ++j) {
           enqueue_p1_step(op, j, (int)k, op->d_V + (size_t)(j - 1) * op->n);
-          if (reorth && j < (int)k) enqueue_reorth(op, j);
+          if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
         }
         d = fetch_decomp(op, k);
         bool go = true;
@@ -987,6 +999,8 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
     if (d.steps > 1) std::memcpy(betas, d.betas, (d.steps - 1) * sizeof(double));
     *steps = d.steps;
     *b_norm = d.b_norm;
+    op->reorth_second =
+        reorth == 2 ? d.flags[3] : (reorth == 1 && d.steps > 1 ? (int64_t)d.steps - 1 : 0);
     if (v_out && d.steps > 0) {
       download_vec(op, v_out, op->d_V, (int64_t)d.steps * op->n, mem);
       sync_checked(op);
@@ -1178,6 +1192,13 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
     case TPL_KERNEL_PASS2_SPMV: return spmv + 8.0 * n + 16.0 * n / 3.0;
     default: return 0.0;
   }
+}
+
+tpl_status tpl_op_reorth_second_passes(tpl_op_t op, int64_t* count) {
+  return guarded([&] {
+    if (!op || !count) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    *count = op->reorth_second;
+  });
 }
 
 tpl_status tpl_op_device_bytes(tpl_op_t op, uint64_t* bytes) {

@@ -83,14 +83,25 @@ def _op(operator) -> HipCsrOp:
     return operator
 
 
+def _reorth_mode(r) -> int:
+    if r in (False, None, 0):
+        return 0
+    if r in (True, 1, "cgs2"):
+        return 1
+    if r in (2, "selective"):
+        return 2
+    raise ValueError("reorthogonalize must be False, True / 'cgs2' or 'selective'")
+
+
 def lanczos_standard(operator, b, k: int, callback: Optional[Callable] = None,
-                     reorthogonalize: bool = False) -> LanczosOutput:
+                     reorthogonalize=False) -> LanczosOutput:
     """One-pass Lanczos storing V_k (in HBM); src/algorithms/lanczos.rs:55-156.
 
     ``callback(k, v_k_view, t_k_view) -> bool`` mirrors ``LanczosCallback``
     (src/algorithms/mod.rs:82-86): return False to stop early.
-    ``reorthogonalize=True`` adds CGS2 full re-orthogonalisation against V_k —
-    an extension with no reference counterpart (not used by any reference path).
+    ``reorthogonalize=True`` (or ``"cgs2"``) adds CGS2 full re-orthogonalisation against
+    V_k, ``"selective"`` the Kahan–Parlett variant (second pass only when needed) —
+    extensions with no reference counterpart (not used by any reference path).
     """
     op = _op(operator)
     bv = Vec(b)
@@ -115,7 +126,7 @@ def lanczos_standard(operator, b, k: int, callback: Optional[Callable] = None,
     check(_lib.tpl_lanczos_standard(
         op.handle, bv.ptr, bv.n, k, alphas.ctypes.data_as(POINTER(c_double)),
         betas.ctypes.data_as(POINTER(c_double)), byref(steps), byref(bnorm), Vec.ptr_of(v_full),
-        bv.mem, 1 if reorthogonalize else 0, cb_c, None))
+        bv.mem, _reorth_mode(reorthogonalize), cb_c, None))
     if raised:
         raise raised[0]
     s = steps.value

@@ -151,6 +151,12 @@ class HipCsrOp:
         check(_lib.tpl_profile_kernel(self._op, kernel, iters, byref(us), byref(by)))
         return us.value, by.value
 
+    def reorth_second_passes(self) -> int:
+        """Second Gram-Schmidt passes of the last re-orthogonalised lanczos_standard."""
+        v = c_int64()
+        check(_lib.tpl_op_reorth_second_passes(self._op, byref(v)))
+        return int(v.value)
+
     def flags(self) -> int:
         """tpl_op_flags bits (include/tpl.h)."""
         return int(_lib.tpl_op_flags(self._op))
