@@ -84,8 +84,22 @@ int64_t tpl_op_nnz(tpl_op_t op);
  * a host transport, or a transport that refused stream capture); bit 2: values kept
  * as int8, bit 3 / bit 4: short-row / long-row column indices kept as uint16 offsets
  * (see tpl_op_set_value_format), bit 5: the last tpl_lanczos_two_pass ran as one
- * device graph (device f(T_k)). -1 if op is NULL.                                  */
+ * device graph (device f(T_k)), bit 6: rows held in the locality order
+ * (tpl_op_set_reorder). -1 if op is NULL.                                          */
 int tpl_op_flags(tpl_op_t op);
+/* Locality order (single-GPU operators; rebuilds the layout). on != 0 (default): the
+ * device holds P A P^T, the short rows sorted by the long rows (hub columns) they
+ * reference and the long rows last, so the hub rows' gathers touch compact runs;
+ * every vector crossing the boundary (b, x, apply's x / y, V_k, the callback's view)
+ * is permuted on the device, so the caller sees its own row order throughout. The
+ * permutation changes the device's reduction order (summation order within rows and of
+ * the partials): results are bitwise those of the oracle run on P A P^T with the same
+ * schedule, and agree with the unpermuted operator to rounding. No effect when the
+ * matrix has no long rows, and none on row-partitioned operators.                   */
+tpl_status tpl_op_set_reorder(tpl_op_t op, int on);
+/* perm[i] = the caller's row held at internal position i (n entries; the identity
+ * when the operator is not reordered). tpl_op_schedule's row lists are internal.    */
+tpl_status tpl_op_permutation(tpl_op_t op, int32_t* perm);
 /* Storage format (rebuilds the layout): compress != 0 (default) keeps the values as
  * int8 when every one is an integer in [-128, 127] (not -0.0), and the column
  * indices as uint16 offsets from a per-chunk / per-bin base when the spans allow —

@@ -103,10 +103,48 @@ def short_row_threshold(lens, requested=-1):
     return max(4, min(32, 2 * m))
 
 
-def canon_schedule(a, short_row_max=-1, max_g2=1024):
-    """The device's layout rule (two-pass-lanczos_amd/csrc/tpl_runtime.cpp, build_layout)
+def locality_perm(a, short_row_max=-1, groups=16):
+    """tpl_layout.cpp locality_order restated: short rows sorted by (group(lo), group(hi),
+    lo, hi, row) — lo / hi the smallest / largest rank, among the long rows, of a long
+    column the row references (none: after all others), group = rank * groups // n_long —
+    then the long rows ascending. None when that is the identity (or no long rows)."""
+    a = a.tocsr()
+    n = a.shape[0]
+    lens = np.diff(a.indptr)
+    T = short_row_threshold(lens, short_row_max)
+    long_ = np.nonzero(lens > T)[0]
+    if long_.size == 0:
+        return None
+    rank = np.full(n, -1, dtype=np.int64)
+    rank[long_] = np.arange(long_.size)
+    big = np.iinfo(np.int32).max
+    rows = np.repeat(np.arange(n), lens)
+    r = rank[a.indices]
+    m = r >= 0
+    lo = np.full(n, big, dtype=np.int64)
+    hi = np.full(n, -1, dtype=np.int64)
+    np.minimum.at(lo, rows[m], r[m])
+    np.maximum.at(hi, rows[m], r[m])
+    hi[hi < 0] = big
+    grp = lambda x: np.where(x == big, big, x * groups // long_.size)
+    short = np.nonzero(lens <= T)[0]
+    o = np.lexsort((short, hi[short], lo[short], grp(hi[short]), grp(lo[short])))
+    perm = np.concatenate([short[o], long_]).astype(np.int32)
+    return None if np.array_equal(perm, np.arange(n)) else perm
+
+
+def canon_schedule(a, short_row_max=-1, max_g2=1024, reorder=False):
+    """The device's layout rule (two-pass-lanczos_amd/csrc/tpl_layout.cpp, build_layout)
     restated, for oracle runs without a GPU. The GPU tests take the layout from the
-    live operator instead (HipCsrOp.schedule())."""
+    live operator instead (HipCsrOp.schedule()). reorder: the single-GPU operator's
+    default locality order (tpl_op_set_reorder) — the rule is then applied to P A P^T and
+    the schedule carries "perm"."""
+    if reorder:
+        perm = locality_perm(a, short_row_max)
+        if perm is not None:
+            s = canon_schedule(a.tocsr()[perm][:, perm].tocsr(), short_row_max, max_g2)
+            s["perm"] = perm
+            return s
     rp = a.indptr
     n = a.shape[0]
     lens = np.diff(rp)
@@ -117,7 +155,7 @@ def canon_schedule(a, short_row_max=-1, max_g2=1024):
     per = -(-n // g2)
     E = max(512, (per + 511) // 512 * 512)
     return {"short_rows": short, "long_rows": long_, "G2": g2, "E": E,
-            "slices": auto_slices(a, long_)}
+            "slices": auto_slices(a, long_), "perm": None}
 
 
 def auto_slices(a, long_rows, bin_max=7936):

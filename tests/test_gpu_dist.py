@@ -48,6 +48,7 @@ def _single(kkt_tmp, arcs=5000, k=50):
     a = load_kkt(arcs, kkt_tmp).a
     b = harness_b(a)
     op = tpl_amd.HipCsrOp(a)
+    op.set_reorder(False)  # partitioned operators keep the caller's row order
     return (a, tpl_amd.lanczos_two_pass(op, b, k, "inv"),
             tpl_amd.algorithms.lanczos_pass_one(op, b, k), tpl_amd.lanczos(op, b, k, "inv"))
 

@@ -359,6 +359,17 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
   }
 }
 
+// Row permutation at the boundary (locality order, tpl_layout.h): out[i] = in[idx[i]] for
+// each of `cols` columns (leading dimensions ldo / ldi).
+__global__ __launch_bounds__(kTPB) void k_permute(int64_t n, int cols, double* __restrict__ out,
+                                                  int64_t ldo, const double* __restrict__ in,
+                                                  int64_t ldi, const int32_t* __restrict__ idx) {
+  const int c = blockIdx.y;
+  for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n;
+       i += (int64_t)gridDim.x * kTPB)
+    out[(int64_t)c * ldo + i] = in[(int64_t)c * ldi + idx[i]];
+}
+
 // ---------------------------------------- replicated long rows (partitioned solve)
 // Long row l = sum over ranks, in rank order, of the R partials all-gathered into
 // yall[r * n_long + l]; every rank then runs the row's epilogue (identical bits on all
@@ -659,6 +670,15 @@ hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const do
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, int dyn, hipStream_t s) {
   hipLaunchKernelGGL(k_p2_init, dim3(elem_grid(n)), dim3(kTPB), 0, s, n, S, b, v1, x, Vcol, dyn);
+  return hipGetLastError();
+}
+hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
+                   const int32_t* idx, hipStream_t s) {
+  for (int c0 = 0; n > 0 && c0 < cols; c0 += 65535) {
+    const int c = std::min(cols - c0, 65535);
+    hipLaunchKernelGGL(k_permute, dim3(elem_grid(n), c), dim3(kTPB), 0, s, n, c,
+                       out + (int64_t)c0 * ldo, ldo, in + (int64_t)c0 * ldi, ldi, idx);
+  }
   return hipGetLastError();
 }
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s) {

@@ -45,10 +45,79 @@ int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int reque
   return std::max<int32_t>(4, std::min<int32_t>(kShortRowMax, 2 * median));
 }
 
+std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
+                                    const std::vector<int32_t>& col, const SchedParams& sp) {
+  const int32_t T = short_row_threshold(n, rp, sp.short_row_max);
+  std::vector<int32_t> rank(n, -1);  // long row -> its rank among the long rows
+  int32_t n_long = 0;
+  for (int64_t i = 0; i < n; ++i) {
+    const bool is_long = sp.long_from >= 0 ? i >= sp.long_from : rp[i + 1] - rp[i] > T;
+    if (is_long) rank[i] = n_long++;
+  }
+  if (n_long == 0) return {};
+  struct Key {
+    int32_t glo, ghi, rlo, rhi, row;
+  };
+  std::vector<Key> keys;
+  keys.reserve(n - n_long);
+  for (int64_t i = 0; i < n; ++i) {
+    if (rank[i] >= 0) continue;
+    int32_t lo = INT32_MAX, hi = INT32_MAX;  // no long reference: after the others
+    for (int32_t q = rp[i]; q < rp[i + 1]; ++q) {
+      const int32_t r = rank[col[q]];
+      if (r < 0) continue;
+      if (lo == INT32_MAX) lo = r;
+      hi = r;  // columns ascend and ranks follow the row order
+    }
+    auto grp = [&](int32_t r) {
+      return r == INT32_MAX ? INT32_MAX : (int32_t)((int64_t)r * kOrderGroups / n_long);
+    };
+    keys.push_back(Key{grp(lo), grp(hi), lo, hi, (int32_t)i});
+  }
+  std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+    if (x.glo != y.glo) return x.glo < y.glo;
+    if (x.ghi != y.ghi) return x.ghi < y.ghi;
+    if (x.rlo != y.rlo) return x.rlo < y.rlo;
+    if (x.rhi != y.rhi) return x.rhi < y.rhi;
+    return x.row < y.row;
+  });
+  std::vector<int32_t> perm;
+  perm.reserve(n);
+  for (const Key& k : keys) perm.push_back(k.row);
+  for (int64_t i = 0; i < n; ++i)
+    if (rank[i] >= 0) perm.push_back((int32_t)i);
+  bool identity = true;
+  for (int64_t i = 0; i < n && identity; ++i) identity = perm[i] == i;
+  if (identity) return {};
+  return perm;
+}
 
-// n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds
-// are taken on global column indices, so a partition of one rank reproduces the
-// single-GPU layout exactly).
+void permute_csr(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& col,
+                 const std::vector<double>& val, const std::vector<int32_t>& perm,
+                 const std::vector<int32_t>& iperm, std::vector<int32_t>& prp,
+                 std::vector<int32_t>& pcol, std::vector<double>& pval) {
+  prp.assign(1, 0);
+  pcol.clear();
+  pval.clear();
+  pcol.reserve(col.size());
+  pval.reserve(val.size());
+  std::vector<std::pair<int32_t, double>> row;
+  for (int64_t i = 0; i < n; ++i) {
+    const int32_t e = perm[i];
+    row.clear();
+    for (int32_t q = rp[e]; q < rp[e + 1]; ++q) row.emplace_back(iperm[col[q]], val[q]);
+    std::sort(row.begin(), row.end(),
+              [](const std::pair<int32_t, double>& a, const std::pair<int32_t, double>& b) {
+                return a.first < b.first;
+              });
+    for (const auto& x : row) {
+      pcol.push_back(x.first);
+      pval.push_back(x.second);
+    }
+    prp.push_back((int32_t)pcol.size());
+  }
+}
+
 Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
                            const std::vector<int32_t>& col, const std::vector<double>& val,
                            const SchedParams& sp, const ColMap& cmap) {

@@ -63,6 +63,25 @@ struct ColMap {
 // 4, kShortRowMax).
 int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int requested);
 
+// Locality order of the rows (an internal symmetric permutation, single-GPU operators):
+// perm[i] = the caller's row placed at internal position i, or an empty vector when
+// the order would not change (no long rows). Short rows first, keyed by the long
+// columns they reference — (group(lo), group(hi), rank(lo), rank(hi), row) with lo / hi
+// the smallest / largest referenced long column, rank = its position among the long
+// rows and group = rank * kOrderGroups / n_long — then the long rows, ascending. For the
+// KKT matrices this orders the arcs by (endpoint group, endpoint group, endpoints):
+// the arcs of each node then lie in a few compact runs, so the long-row bins' gathers
+// of a node's arcs hit lines their neighbours have just fetched.
+constexpr int kOrderGroups = 16;
+std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
+                                    const std::vector<int32_t>& col, const SchedParams& sp);
+// P A P^T in CSR: internal row i = the caller's row perm[i], columns mapped through
+// iperm (the inverse) and re-sorted ascending.
+void permute_csr(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& col,
+                 const std::vector<double>& val, const std::vector<int32_t>& perm,
+                 const std::vector<int32_t>& iperm, std::vector<int32_t>& prp,
+                 std::vector<int32_t>& pcol, std::vector<double>& pval);
+
 // n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds are
 // taken on global column indices, so a partition of one rank reproduces the single-GPU
 // layout exactly). Throws tpl::Error (TPL_ERR_UNSUPPORTED) for layouts the device

@@ -35,6 +35,8 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s);
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
+hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
+                   const int32_t* idx, hipStream_t s);
 hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, int dyn, hipStream_t s);
@@ -185,6 +187,16 @@ struct tpl_op_s {
   int device_ftk = 2;               // built-in inv on the device (one graph): 0 off, 1 on, 2 auto
   bool last_one_graph = false;      // the last tpl_lanczos_two_pass ran as one device graph
   int64_t reorth_second = 0;        // second Gram-Schmidt passes of the last reorth solve
+  // locality order (single GPU, tpl_op_set_reorder): the device works on P A P^T; vectors
+  // cross the boundary through a gather (internal i <- caller's perm[i], back via iperm).
+  // h_rowptr / h_col / h_val keep the caller's order.
+  bool reorder = true;
+  std::vector<int32_t> perm, iperm;
+  int32_t* d_perm = nullptr;
+  int32_t* d_iperm = nullptr;
+  double* d_stage = nullptr;        // one host-order vector (host uploads / downloads)
+  double* d_Vext = nullptr;         // the callback's V_k view in the caller's order
+  size_t vext_cols = 0;
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
 };
@@ -275,11 +287,28 @@ void rebuild_schedule(tpl_op_s* op) {
     cmap.starts = &op->starts;
     cmap.ld = op->ld;
   }
+  op->perm.clear();
+  op->iperm.clear();
+  if (op->reorder && !op->dist) op->perm = locality_order(op->n, op->h_rowptr, op->h_col, op->sp);
+  std::vector<int32_t> prp, pcol;
+  std::vector<double> pval;
+  if (!op->perm.empty()) {
+    op->iperm.resize(op->n);
+    for (int64_t i = 0; i < op->n; ++i) op->iperm[op->perm[i]] = (int32_t)i;
+    permute_csr(op->n, op->h_rowptr, op->h_col, op->h_val, op->perm, op->iperm, prp, pcol, pval);
+  }
+  const bool p = !op->perm.empty();
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
-  op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, op->h_rowptr, op->h_col,
-                         op->h_val, op->sp, cmap);
+  op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
+                         p ? pcol : op->h_col, p ? pval : op->h_val, op->sp, cmap);
   const Layout& L = op->lay;
+  upload(op, &op->d_perm, op->perm);
+  upload(op, &op->d_iperm, op->iperm);
+  dev_free(op, op->d_stage);
+  dev_free(op, op->d_Vext);
+  op->vext_cols = 0;
+  if (p) dev_alloc(op, &op->d_stage, (size_t)op->n * sizeof(double));
   upload(op, &op->d_srows, L.srows);
   if (L.s_col16)
     upload(op, reinterpret_cast<uint16_t**>(&op->d_scol), L.s_col16v);
@@ -367,17 +396,45 @@ void check_b(const tpl_op_s* op, const double* b, int64_t b_len) {
   if (b_len != op->n) fail(TPL_ERR_DIMENSION_MISMATCH, msg_dimension(op->n, b_len));
 }
 
+// A caller-order vector into a device vector (internal order).
 void upload_vec(tpl_op_s* op, double* dst, const double* src, int mem) {
   if (op->n == 0) return;
-  HIPCHK(hipMemcpyAsync(dst, src, op->n * sizeof(double),
-                        mem == TPL_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
-                        op->stream));
+  const size_t bytes = op->n * sizeof(double);
+  if (!op->d_perm) {
+    HIPCHK(hipMemcpyAsync(dst, src, bytes,
+                          mem == TPL_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice,
+                          op->stream));
+    return;
+  }
+  const double* from = src;
+  if (mem != TPL_MEM_DEVICE) {
+    HIPCHK(hipMemcpyAsync(op->d_stage, src, bytes, hipMemcpyHostToDevice, op->stream));
+    from = op->d_stage;
+  }
+  HIPCHK(launch::permute(op->n, 1, dst, op->n, from, op->n, op->d_perm, op->stream));
 }
-void download_vec(tpl_op_s* op, double* dst, const double* src, int64_t count, int mem) {
-  if (count == 0) return;
-  HIPCHK(hipMemcpyAsync(dst, src, count * sizeof(double),
-                        mem == TPL_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
-                        op->stream));
+// `cols` device columns (internal order, ld = n) out to the caller, in the caller's order.
+void download_vec(tpl_op_s* op, double* dst, const double* src, int64_t cols, int mem) {
+  if (cols == 0 || op->n == 0) return;
+  // one vector, or columns of the basis: nothing else is ever this wide
+  if (cols < 0 || (cols > 1 && (src != op->d_V || (size_t)cols > op->vcols)))
+    fail(TPL_ERR_INVALID_ARGUMENT, "download_vec: column count exceeds its source");
+  if (!op->d_perm) {
+    HIPCHK(hipMemcpyAsync(dst, src, cols * op->n * sizeof(double),
+                          mem == TPL_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                          op->stream));
+    return;
+  }
+  if (mem == TPL_MEM_DEVICE) {
+    HIPCHK(launch::permute(op->n, (int)cols, dst, op->n, src, op->n, op->d_iperm, op->stream));
+    return;
+  }
+  for (int64_t c = 0; c < cols; ++c) {  // through the staging vector, a column at a time
+    HIPCHK(launch::permute(op->n, 1, op->d_stage, op->n, src + c * op->n, op->n, op->d_iperm,
+                           op->stream));
+    HIPCHK(hipMemcpyAsync(dst + c * op->n, op->d_stage, op->n * sizeof(double),
+                          hipMemcpyDeviceToHost, op->stream));
+  }
 }
 
 // r_j buffer of pass one: r_1 = b, then R[j % 3] (local view, and gather source).
@@ -862,19 +919,8 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     hipSetDevice(op->device);
     hipStreamSynchronize(op->stream);
     drop_graphs(op);
-    for (void* p : {(void*)op->d_bcol, (void*)op->d_bval, (void*)op->d_bseg, (void*)op->d_bhdr, (void*)op->d_P,
-                    (void*)op->d_Pcnt,
-                    (void*)op->d_bcbase, (void*)op->d_scbase,
-                    (void*)op->d_srows, (void*)op->d_scol, (void*)op->d_sval,
-                    (void*)op->d_cbase, (void*)op->d_cwidth})
-      if (p) hipFree(p);
-    hipFree(op->d_vecs);
-    if (op->d_rsum) hipFree(op->d_rsum);
-    if (op->d_yall) hipFree(op->d_yall);
-    if (op->d_state) hipFree(op->d_state);
+    for (const auto& kv : op->allocs) hipFree(const_cast<void*>(kv.first));  // every dev_alloc
     if (op->h_state) hipHostFree(op->h_state);
-    if (op->d_Pr) hipFree(op->d_Pr);
-    if (op->d_V) hipFree(op->d_V);
     if (op->ev0) hipEventDestroy(op->ev0);
     if (op->ev1) hipEventDestroy(op->ev1);
     for (hipEvent_t e : op->tev)
@@ -887,7 +933,28 @@ int64_t tpl_op_nrows(tpl_op_t op) { return op ? op->n : -1; }
 int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
   return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0) |
-         (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0) | (op->last_one_graph ? 32 : 0);
+         (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0) | (op->last_one_graph ? 32 : 0) |
+         (op->d_perm ? 64 : 0);
+}
+
+tpl_status tpl_op_set_reorder(tpl_op_t op, int on) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    set_device(op);
+    sync_checked(op);
+    op->reorder = on != 0;
+    rebuild_schedule(op);
+  });
+}
+
+tpl_status tpl_op_permutation(tpl_op_t op, int32_t* perm) {
+  return guarded([&] {
+    if (!op || (!perm && op->n > 0)) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (op->perm.empty())
+      for (int64_t i = 0; i < op->n; ++i) perm[i] = (int32_t)i;
+    else
+      std::copy(op->perm.begin(), op->perm.end(), perm);
+  });
 }
 
 tpl_status tpl_op_set_value_format(tpl_op_t op, int compress) {
@@ -915,7 +982,7 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
       dist_allgather(op, op->d_yall, (size_t)A.n_long);
       HIPCHK(launch::long_epi_y(A, op->d_yall, op->dist->nranks, op->W, op->stream));
     }
-    download_vec(op, y, op->W, op->n, mem);
+    download_vec(op, y, op->W, 1, mem);
     sync_checked(op);
   });
 }
@@ -965,6 +1032,18 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
       // result, with one host synchronisation per batch instead of per step.
       ensure_state(op, k, reorth != 0);
       ensure_basis(op, k);
+      // the callback's view in the caller's row order: each batch's new columns are
+      // gathered into d_Vext (an n x k buffer, reordered operators only)
+      double* Vview = op->d_V;
+      if (op->d_perm) {
+        if (op->vext_cols < k) {
+          dev_free(op, op->d_Vext);
+          op->vext_cols = 0;
+          dev_alloc(op, &op->d_Vext, (size_t)op->n * k * sizeof(double));
+          op->vext_cols = k;
+        }
+        Vview = op->d_Vext;
+      }
       upload_vec(op, op->b, b, mem);
       enqueue_p1_prologue(op);
       size_t stop_at = k;
@@ -975,6 +1054,10 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
           enqueue_p1_step(op, j, (int)k, op->d_V + (size_t)(j - 1) * op->n);
           if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
         }
+        if (Vview != op->d_V)
+          HIPCHK(launch::permute(op->n, j1 - j0 + 1, Vview + (size_t)(j0 - 1) * op->n, op->n,
+                                 op->d_V + (size_t)(j0 - 1) * op->n, op->n, op->d_iperm,
+                                 op->stream));
         d = fetch_decomp(op, k);
         bool go = true;
         for (int j = j0; j <= j1 && go; ++j) {
@@ -983,7 +1066,7 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
             go = false;
             break;
           }
-          go = cb((size_t)j, op->d_V, op->n, d.alphas, (size_t)j, d.betas, (size_t)j - 1,
+          go = cb((size_t)j, Vview, op->n, d.alphas, (size_t)j, d.betas, (size_t)j - 1,
                   cb_user) != 0;
           if (!go) stop_at = (size_t)j;
         }
@@ -1002,7 +1085,7 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
     op->reorth_second =
         reorth == 2 ? d.flags[3] : (reorth == 1 && d.steps > 1 ? (int64_t)d.steps - 1 : 0);
     if (v_out && d.steps > 0) {
-      download_vec(op, v_out, op->d_V, (int64_t)d.steps * op->n, mem);
+      download_vec(op, v_out, op->d_V, (int64_t)d.steps, mem);
       sync_checked(op);
     }
   });
@@ -1045,8 +1128,8 @@ tpl_status tpl_lanczos_pass_two(tpl_op_t op, const double* b, int64_t b_len, con
     } else {
       run_pass2(op, steps);
     }
-    download_vec(op, x_out, op->x, op->n, mem);
-    if (v_out) download_vec(op, v_out, op->d_V, (int64_t)steps * op->n, mem);
+    download_vec(op, x_out, op->x, 1, mem);
+    if (v_out) download_vec(op, v_out, op->d_V, (int64_t)steps, mem);
     sync_checked(op);
   });
 }
@@ -1066,7 +1149,7 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
       upload_vec(op, op->b, b, mem);
       op->last_one_graph = true;
       run_two_pass_dev(op, k);
-      download_vec(op, x_out, op->x, op->n, mem);
+      download_vec(op, x_out, op->x, 1, mem);
       HIPCHK(hipMemcpyAsync(op->h_state, op->d_state, 16, hipMemcpyDeviceToHost, op->stream));
       sync_checked(op);
       int32_t flags[4];
@@ -1093,7 +1176,7 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
                           op->stream));
     // 4. pass two (:174)
     run_pass2(op, d.steps);
-    download_vec(op, x_out, op->x, op->n, mem);
+    download_vec(op, x_out, op->x, 1, mem);
     sync_checked(op);
   });
 }
@@ -1120,7 +1203,7 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
                           op->stream));
     // 3. x = ||b|| V_k y' (:96-104)
     HIPCHK(launch::gemv_recon(op->n, (int)d.steps, op->S, op->d_V, op->x, op->stream));
-    download_vec(op, x_out, op->x, op->n, mem);
+    download_vec(op, x_out, op->x, 1, mem);
     sync_checked(op);
   });
 }

@@ -116,6 +116,8 @@ tpl_op_enable_timing = _sig("tpl_op_enable_timing", c_int, c_void_p, c_int)
 tpl_op_pass_timing = _sig("tpl_op_pass_timing", c_int, c_void_p, PD, PD, POINTER(c_int64))
 tpl_op_set_device_ftk = _sig("tpl_op_set_device_ftk", c_int, c_void_p, c_int)
 tpl_op_device_bytes = _sig("tpl_op_device_bytes", c_int, c_void_p, POINTER(ctypes.c_uint64))
+tpl_op_set_reorder = _sig("tpl_op_set_reorder", c_int, c_void_p, c_int)
+tpl_op_permutation = _sig("tpl_op_permutation", c_int, c_void_p, POINTER(c_int32))
 tpl_op_reorth_second_passes = _sig("tpl_op_reorth_second_passes", c_int, c_void_p, POINTER(c_int64))
 
 # built-in f(T_k) solvers: raw C function pointers usable as tpl_ftk_fn
@@ -139,7 +141,8 @@ EXPORTED = [
     "tpl_op_set_schedule", "tpl_op_slices", "tpl_op_set_slices", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
     "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_generate_kkt", "tpl_op_flags",
     "tpl_op_set_value_format", "tpl_op_set_device_ftk",
-    "tpl_op_device_bytes", "tpl_op_reorth_second_passes",
+    "tpl_op_device_bytes", "tpl_op_reorth_second_passes", "tpl_op_set_reorder",
+    "tpl_op_permutation",
 ]
 
 

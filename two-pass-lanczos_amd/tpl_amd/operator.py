@@ -124,8 +124,9 @@ class HipCsrOp:
 
     # -- schedule / measurement ------------------------------------------------
     def schedule(self):
-        """Device layout: dict(short_rows, long_rows, G2, E, slices) —
-        what the oracle needs to reproduce the device reduction order."""
+        """Device layout: dict(short_rows, long_rows, G2, E, slices, perm) — what the
+        oracle needs to reproduce the device reduction order. Row lists are internal
+        indices; perm[i] = the caller's row at internal position i (None: identity)."""
         ns, nl, g2, e = c_int32(), c_int32(), c_int32(), c_int64()
         check(_lib.tpl_op_schedule(self._op, byref(ns), byref(nl), byref(g2), byref(e), None, None))
         sr = np.zeros(max(ns.value, 1), dtype=np.int32)
@@ -135,8 +136,19 @@ class HipCsrOp:
                                    lr.ctypes.data_as(POINTER(c_int32))))
         sl = c_int32()
         check(_lib.tpl_op_slices(self._op, byref(sl)))
+        n = int(_lib.tpl_op_nrows(self._op))
+        perm = np.zeros(max(n, 1), dtype=np.int32)
+        check(_lib.tpl_op_permutation(self._op, perm.ctypes.data_as(POINTER(c_int32))))
+        perm = perm[:n]
+        ident = bool(np.array_equal(perm, np.arange(n, dtype=np.int32)))
         return {"short_rows": sr[:ns.value].copy(), "long_rows": lr[:nl.value].copy(),
-                "G2": g2.value, "E": e.value, "slices": sl.value}
+                "G2": g2.value, "E": e.value, "slices": sl.value,
+                "perm": None if ident else perm.copy()}
+
+    def set_reorder(self, on: bool = True):
+        """Locality row order on the device (default on; rebuilds the layout). The
+        caller's row order is kept at the boundary either way."""
+        check(_lib.tpl_op_set_reorder(self._op, 1 if on else 0))
 
     def set_schedule(self, short_row_max=0, max_g2=0):
         check(_lib.tpl_op_set_schedule(self._op, short_row_max, max_g2))
