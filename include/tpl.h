@@ -87,16 +87,18 @@ int64_t tpl_op_nnz(tpl_op_t op);
  * device graph (device f(T_k)), bit 6: rows held in the locality order
  * (tpl_op_set_reorder). -1 if op is NULL.                                          */
 int tpl_op_flags(tpl_op_t op);
-/* Locality order (single-GPU operators; rebuilds the layout). on != 0 (default): the
- * device holds P A P^T, the short rows sorted by the long rows (hub columns) they
- * reference and the long rows last, so the hub rows' gathers touch compact runs;
+/* Locality order (single-GPU operators; rebuilds the layout). mode 1: the device
+ * holds P A P^T, the short rows sorted by the long rows (hub columns) they reference
+ * and the long rows last, so the hub rows' gathers touch compact runs; mode 0: the
+ * caller's order; mode 2 (default, auto): on up to 2^20 rows (measured gain at the
+ * 500k-arc KKT, none from 1M arcs, a loss at 5M arcs: DESIGN.md §3);
  * every vector crossing the boundary (b, x, apply's x / y, V_k, the callback's view)
  * is permuted on the device, so the caller sees its own row order throughout. The
  * permutation changes the device's reduction order (summation order within rows and of
  * the partials): results are bitwise those of the oracle run on P A P^T with the same
  * schedule, and agree with the unpermuted operator to rounding. No effect when the
  * matrix has no long rows, and none on row-partitioned operators.                   */
-tpl_status tpl_op_set_reorder(tpl_op_t op, int on);
+tpl_status tpl_op_set_reorder(tpl_op_t op, int mode);
 /* perm[i] = the caller's row held at internal position i (n entries; the identity
  * when the operator is not reordered). tpl_op_schedule's row lists are internal.    */
 tpl_status tpl_op_permutation(tpl_op_t op, int32_t* perm);

@@ -104,10 +104,11 @@ def short_row_threshold(lens, requested=-1):
 
 
 def locality_perm(a, short_row_max=-1, groups=16):
-    """tpl_layout.cpp locality_order restated: short rows sorted by (group(lo), group(hi),
-    lo, hi, row) — lo / hi the smallest / largest rank, among the long rows, of a long
-    column the row references (none: after all others), group = rank * groups // n_long —
-    then the long rows ascending. None when that is the identity (or no long rows)."""
+    """tpl_layout.cpp locality_order restated: short rows sorted by (tail, group(lo),
+    group(hi), lo, hi, row) — lo / hi the smallest / largest rank, among the long rows, of
+    a long column the row references (none: after all others), group = rank * groups //
+    n_long, tail = the row references another short row — then the long rows ascending.
+    None when that is the identity (or no long rows)."""
     a = a.tocsr()
     n = a.shape[0]
     lens = np.diff(a.indptr)
@@ -126,9 +127,11 @@ def locality_perm(a, short_row_max=-1, groups=16):
     np.minimum.at(lo, rows[m], r[m])
     np.maximum.at(hi, rows[m], r[m])
     hi[hi < 0] = big
+    tail = np.zeros(n, dtype=np.int64)
+    np.maximum.at(tail, rows, ((r < 0) & (a.indices != rows)).astype(np.int64))
     grp = lambda x: np.where(x == big, big, x * groups // long_.size)
     short = np.nonzero(lens <= T)[0]
-    o = np.lexsort((short, hi[short], lo[short], grp(hi[short]), grp(lo[short])))
+    o = np.lexsort((short, hi[short], lo[short], grp(hi[short]), grp(lo[short]), tail[short]))
     perm = np.concatenate([short[o], long_]).astype(np.int32)
     return None if np.array_equal(perm, np.arange(n)) else perm
 

@@ -61,6 +61,7 @@ def kkt5m(kkt_tmp):
 @pytest.fixture(scope="module")
 def op5m(kkt5m):
     op = HipCsrOp(kkt5m.a)
+    assert not op.flags() & 64  # auto locality order: off above 2^20 rows
     yield op
     op.close()
 

@@ -151,6 +151,18 @@ def test_device_memory_vectors(ops):
     assert same_bits(out_d.v_k.cpu().numpy(), np.asarray(out_h.v_k))
 
 
+def test_modes(kkt5k):
+    op = HipCsrOp(kkt5k.a)
+    assert op.flags() & 64                       # auto: on below 2^20 rows
+    with pytest.raises(Exception):
+        op.set_reorder(3)
+    op.set_reorder(0)
+    assert not op.flags() & 64
+    op.set_reorder(2)
+    assert op.flags() & 64
+    op.close()
+
+
 def test_toggle_rebuilds(kkt5k):
     a = kkt5k.a
     op = HipCsrOp(a)

@@ -56,25 +56,30 @@ std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
   }
   if (n_long == 0) return {};
   struct Key {
-    int32_t glo, ghi, rlo, rhi, row;
+    int32_t tail, glo, ghi, rlo, rhi, row;
   };
   std::vector<Key> keys;
   keys.reserve(n - n_long);
   for (int64_t i = 0; i < n; ++i) {
     if (rank[i] >= 0) continue;
     int32_t lo = INT32_MAX, hi = INT32_MAX;  // no long reference: after the others
+    int32_t tail = 0;
     for (int32_t q = rp[i]; q < rp[i + 1]; ++q) {
       const int32_t r = rank[col[q]];
-      if (r < 0) continue;
+      if (r < 0) {
+        tail |= col[q] != i;  // references another short row
+        continue;
+      }
       if (lo == INT32_MAX) lo = r;
       hi = r;  // columns ascend and ranks follow the row order
     }
     auto grp = [&](int32_t r) {
       return r == INT32_MAX ? INT32_MAX : (int32_t)((int64_t)r * kOrderGroups / n_long);
     };
-    keys.push_back(Key{grp(lo), grp(hi), lo, hi, (int32_t)i});
+    keys.push_back(Key{tail, grp(lo), grp(hi), lo, hi, (int32_t)i});
   }
   std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+    if (x.tail != y.tail) return x.tail < y.tail;
     if (x.glo != y.glo) return x.glo < y.glo;
     if (x.ghi != y.ghi) return x.ghi < y.ghi;
     if (x.rlo != y.rlo) return x.rlo < y.rlo;
@@ -293,7 +298,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   L.b_col16 = compress_cols(L.b_col, (int64_t)L.nslices * L.M, L.bin_cap, L.b_col16v, L.b_cbase);
   // Column window of the short chunks: every chunk's columns within kWinMax of its base
   // (uint16 columns, uniform width 1..4) -> staged in LDS.
-  if (L.s_col16 && L.s_width >= 1 && L.s_width <= 4) {
+  if (sp.window && L.s_col16 && L.s_width >= 1 && L.s_width <= 4) {
     const int64_t per = (int64_t)L.s_width * kChunkRows;
     int32_t win = 0, hi = 0;
     for (int64_t c = 0; c < nchunks; ++c)

@@ -17,6 +17,7 @@ struct SchedParams {
   bool compress_values = true;      // int8 values when all values are small integers
   bool compress_cols = true;        // uint16 column offsets when the spans allow
   int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
+  bool window = true;               // stage the short chunks' column window in LDS
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
@@ -66,9 +67,12 @@ int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int reque
 // Locality order of the rows (an internal symmetric permutation, single-GPU operators):
 // perm[i] = the caller's row placed at internal position i, or an empty vector when
 // the order would not change (no long rows). Short rows first, keyed by the long
-// columns they reference — (group(lo), group(hi), rank(lo), rank(hi), row) with lo / hi
-// the smallest / largest referenced long column, rank = its position among the long
-// rows and group = rank * kOrderGroups / n_long — then the long rows, ascending. For the
+// columns they reference — (tail, group(lo), group(hi), rank(lo), rank(hi), row) with
+// lo / hi the smallest / largest referenced long column, rank = its position among the
+// long rows, group = rank * kOrderGroups / n_long, and tail = 1 for rows that also
+// reference another short row (they go last, next to the long columns, so the chunks
+// that hold them keep the narrow column spans of uint16 columns and the LDS window) —
+// then the long rows, ascending. For the
 // KKT matrices this orders the arcs by (endpoint group, endpoint group, endpoints):
 // the arcs of each node then lie in a few compact runs, so the long-row bins' gathers
 // of a node's arcs hit lines their neighbours have just fetched.

@@ -123,6 +123,10 @@ constexpr size_t kDevFtkMaxK = 1365;
 // (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
 // ~15-25 us (sync, host solve, upload, launch): one graph pays up to k ~ 128.
 constexpr size_t kDevFtkAutoK = 128;
+// Locality order, auto mode: on up to this many rows. Measured k_p2_spmv (KKT, D = 0):
+// 500k arcs 8.4 -> 7.0-7.6 us; 1M and 2M arcs within +-4 %; 5M arcs 54 -> 58 us
+// (the gathered vector, 40 MB, no longer fits the XCDs' L2s; profiles/r02_order_lab.txt).
+constexpr int64_t kReorderAutoMaxRows = 1 << 20;
 }
 
 struct tpl_op_s {
@@ -190,7 +194,7 @@ struct tpl_op_s {
   // locality order (single GPU, tpl_op_set_reorder): the device works on P A P^T; vectors
   // cross the boundary through a gather (internal i <- caller's perm[i], back via iperm).
   // h_rowptr / h_col / h_val keep the caller's order.
-  bool reorder = true;
+  int reorder = 2;                  // 0 off, 1 on, 2 auto (n <= kReorderAutoMaxRows)
   std::vector<int32_t> perm, iperm;
   int32_t* d_perm = nullptr;
   int32_t* d_iperm = nullptr;
@@ -289,7 +293,8 @@ void rebuild_schedule(tpl_op_s* op) {
   }
   op->perm.clear();
   op->iperm.clear();
-  if (op->reorder && !op->dist) op->perm = locality_order(op->n, op->h_rowptr, op->h_col, op->sp);
+  const bool want = op->reorder == 1 || (op->reorder == 2 && op->n <= kReorderAutoMaxRows);
+  if (want && !op->dist) op->perm = locality_order(op->n, op->h_rowptr, op->h_col, op->sp);
   std::vector<int32_t> prp, pcol;
   std::vector<double> pval;
   if (!op->perm.empty()) {
@@ -298,10 +303,15 @@ void rebuild_schedule(tpl_op_s* op) {
     permute_csr(op->n, op->h_rowptr, op->h_col, op->h_val, op->perm, op->iperm, prp, pcol, pval);
   }
   const bool p = !op->perm.empty();
+  // In the locality order a chunk's rows share their hub columns, so its gathers hit
+  // few lines and the LDS window costs more than it saves (measured +0.4 us per SpMV at
+  // 500k): window only in the caller's order.
+  SchedParams sp = op->sp;
+  sp.window = !p;
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
-                         p ? pcol : op->h_col, p ? pval : op->h_val, op->sp, cmap);
+                         p ? pcol : op->h_col, p ? pval : op->h_val, sp, cmap);
   const Layout& L = op->lay;
   upload(op, &op->d_perm, op->perm);
   upload(op, &op->d_iperm, op->iperm);
@@ -937,12 +947,13 @@ int tpl_op_flags(tpl_op_t op) {
          (op->d_perm ? 64 : 0);
 }
 
-tpl_status tpl_op_set_reorder(tpl_op_t op, int on) {
+tpl_status tpl_op_set_reorder(tpl_op_t op, int mode) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    if (mode < 0 || mode > 2) fail(TPL_ERR_INVALID_ARGUMENT, "reorder mode must be 0, 1 or 2");
     set_device(op);
     sync_checked(op);
-    op->reorder = on != 0;
+    op->reorder = mode;
     rebuild_schedule(op);
   });
 }

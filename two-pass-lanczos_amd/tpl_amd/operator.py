@@ -145,10 +145,11 @@ class HipCsrOp:
                 "G2": g2.value, "E": e.value, "slices": sl.value,
                 "perm": None if ident else perm.copy()}
 
-    def set_reorder(self, on: bool = True):
-        """Locality row order on the device (default on; rebuilds the layout). The
-        caller's row order is kept at the boundary either way."""
-        check(_lib.tpl_op_set_reorder(self._op, 1 if on else 0))
+    def set_reorder(self, mode=2):
+        """Locality row order on the device (rebuilds the layout): False / 0 off,
+        True / 1 on, 2 auto (default: on up to 2^20 rows). The caller's row order is
+        kept at the boundary either way."""
+        check(_lib.tpl_op_set_reorder(self._op, int(mode)))
 
     def set_schedule(self, short_row_max=0, max_g2=0):
         check(_lib.tpl_op_set_schedule(self._op, short_row_max, max_g2))
