@@ -1400,6 +1400,25 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
 }
 
 
+// ------------------------------------------------------------ locality order
+tpl_status tpl_locality_order(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
+                              int32_t short_row_max, int32_t* perm, int32_t* applied) {
+  return guarded([&] {
+    if (n < 0 || (n > 0 && (!row_ptr || !perm)) || !applied)
+      fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
+    if (n >= INT32_MAX || (n > 0 && row_ptr[n] >= INT32_MAX))
+      fail(TPL_ERR_UNSUPPORTED, "n and nnz must be < 2^31");
+    std::vector<int32_t> rp(n + 1);
+    for (int64_t i = 0; i <= n; ++i) rp[i] = (int32_t)(n > 0 ? row_ptr[i] : 0);
+    std::vector<int32_t> col(col_idx, col_idx + (n > 0 ? row_ptr[n] : 0));
+    SchedParams sp;
+    sp.short_row_max = short_row_max > 0 ? short_row_max : -1;
+    const std::vector<int32_t> p = locality_order(n, rp, col, sp);
+    *applied = p.empty() ? 0 : 1;
+    for (int64_t i = 0; i < n; ++i) perm[i] = p.empty() ? (int32_t)i : p[i];
+  });
+}
+
 // ------------------------------------------------------------ row partition
 tpl_status tpl_dist_partition(int64_t n, const int64_t* row_ptr, int nranks, int64_t* starts) {
   return guarded([&] {

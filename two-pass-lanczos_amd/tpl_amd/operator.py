@@ -57,6 +57,18 @@ def _as_csr_arrays(a):
             m.data.astype(np.float64))
 
 
+def locality_order(a, short_row_max: int = -1):
+    """The device's locality row order for matrix ``a`` (tpl_locality_order; host only):
+    perm[i] = the row held at internal position i, or None when it is the identity."""
+    n, rp, ci, _ = _as_csr_arrays(a)
+    perm = np.zeros(max(n, 1), dtype=np.int32)
+    applied = c_int32()
+    check(_lib.tpl_locality_order(n, rp.ctypes.data_as(POINTER(c_int64)),
+                                  ci.ctypes.data_as(POINTER(c_int32)), int(short_row_max),
+                                  perm.ctypes.data_as(POINTER(c_int32)), byref(applied)))
+    return perm[:n].copy() if applied.value else None
+
+
 def _is_torch_cuda(x) -> bool:
     return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
 
