@@ -102,11 +102,22 @@ tpl_status tpl_op_set_reorder(tpl_op_t op, int mode);
 /* perm[i] = the caller's row held at internal position i (n entries; the identity
  * when the operator is not reordered). tpl_op_schedule's row lists are internal.    */
 tpl_status tpl_op_permutation(tpl_op_t op, int32_t* perm);
+/* Tune the locality order's group count on this device (single GPU; switches the
+ * order on): rebuilds the layout for each of the `count` group counts in `groups`
+ * (count 0: 12..20, 22, 24), times `iters` launches each of the pass-one and pass-two
+ * SpMV kernels, keeps the fastest and reports it in *chosen (*best_us: the sum of the
+ * two kernels' average launch times). The choice depends on measured times, so two
+ * tuned operators of one matrix may hold different orders (each bitwise against the
+ * oracle given its own permutation); untuned operators are deterministic.          */
+tpl_status tpl_op_tune_order(tpl_op_t op, const int32_t* groups, int32_t count, int32_t iters,
+                             int32_t* chosen, double* best_us);
 /* The locality order's rule alone (host only, no device): perm (n entries) as
- * tpl_op_permutation would report it for this CSR (columns ascending per row) and
- * short-row threshold (<= 0: auto); *applied = 0 when the order is the identity.   */
+ * tpl_op_permutation would report it for this CSR (columns ascending per row),
+ * short-row threshold (<= 0: auto) and group count (<= 0: 16); *applied = 0 when the
+ * order is the identity.                                                           */
 tpl_status tpl_locality_order(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
-                              int32_t short_row_max, int32_t* perm, int32_t* applied);
+                              int32_t short_row_max, int32_t groups, int32_t* perm,
+                              int32_t* applied);
 /* Storage format (rebuilds the layout): compress != 0 (default) keeps the values as
  * int8 when every one is an integer in [-128, 127] (not -0.0), and the column
  * indices as uint16 offsets from a per-chunk / per-bin base when the spans allow —

@@ -106,8 +106,9 @@ def short_row_threshold(lens, requested=-1):
 def locality_perm(a, short_row_max=-1, groups=16):
     """tpl_layout.cpp locality_order restated: short rows sorted by (tail, group(lo),
     group(hi), lo, hi, row) — lo / hi the smallest / largest rank, among the long rows, of
-    a long column the row references (none: after all others), group = rank * groups //
-    n_long, tail = the row references another short row — then the long rows ascending.
+    a long column the row references (none: after all others), group = rank //
+    ceil(n_long / groups), tail = the row references another short row — then the long
+    rows ascending.
     None when that is the identity (or no long rows)."""
     a = a.tocsr()
     n = a.shape[0]
@@ -129,7 +130,8 @@ def locality_perm(a, short_row_max=-1, groups=16):
     hi[hi < 0] = big
     tail = np.zeros(n, dtype=np.int64)
     np.maximum.at(tail, rows, ((r < 0) & (a.indices != rows)).astype(np.int64))
-    grp = lambda x: np.where(x == big, big, x * groups // long_.size)
+    gsize = -(-long_.size // groups)
+    grp = lambda x: np.where(x == big, big, x // gsize)
     short = np.nonzero(lens <= T)[0]
     o = np.lexsort((short, hi[short], lo[short], grp(hi[short]), grp(lo[short]), tail[short]))
     perm = np.concatenate([short[o], long_]).astype(np.int32)

@@ -175,3 +175,21 @@ def test_toggle_rebuilds(kkt5k):
     assert same_bits(solvers.lanczos_two_pass(op, b, 30, ftk.INV), x_on)
     assert np.linalg.norm(x_on - x_off) <= 1e-9 * np.linalg.norm(x_off)
     op.close()
+
+
+def test_tune_order(kkt50k):
+    """tpl_op_tune_order keeps one of the candidates, switches the order on, and the
+    tuned operator is bitwise the oracle's on its own permutation."""
+    a = kkt50k.a
+    op = HipCsrOp(a)
+    op.set_reorder(0)
+    g, us = op.tune_order([12, 16, 20], iters=20)
+    assert g in (12, 16, 20) and us > 0 and op.flags() & 64
+    sch = op.schedule()
+    assert np.array_equal(sch["perm"], tpl_amd.locality_order(a, groups=g))
+    b = harness_b(a)
+    o = oracle.Operator(a, sch)
+    assert same_bits(solvers.lanczos_two_pass(op, b, 40, ftk.INV), o.lanczos_two_pass(b, 40, ftk.INV))
+    with pytest.raises(Exception):
+        op.tune_order([0])
+    op.close()

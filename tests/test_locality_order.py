@@ -82,3 +82,11 @@ def test_tail_rows_keep_chunk_spans(kkt_tmp):
     n_short = int(np.sum(lens <= 4))
     tail = set(perm[n_short - 2:n_short].tolist())
     assert n - 1 in tail
+
+
+@pytest.mark.parametrize("groups", [1, 7, 16, 24, 5000])
+def test_group_counts(kkt_tmp, groups):
+    a = load_kkt(50000, kkt_tmp).a
+    got = tpl_amd.locality_order(a, groups=groups)
+    ref = locality_perm(a.tocsr(), groups=groups)
+    assert np.array_equal(got, ref)

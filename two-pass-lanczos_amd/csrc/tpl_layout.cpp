@@ -55,6 +55,8 @@ std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
     if (is_long) rank[i] = n_long++;
   }
   if (n_long == 0) return {};
+  const int32_t G = std::max(1, sp.order_groups);
+  const int32_t gsize = (n_long + G - 1) / G;  // long-row ranks per group
   struct Key {
     int32_t tail, glo, ghi, rlo, rhi, row;
   };
@@ -73,9 +75,7 @@ std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
       if (lo == INT32_MAX) lo = r;
       hi = r;  // columns ascend and ranks follow the row order
     }
-    auto grp = [&](int32_t r) {
-      return r == INT32_MAX ? INT32_MAX : (int32_t)((int64_t)r * kOrderGroups / n_long);
-    };
+    auto grp = [&](int32_t r) { return r == INT32_MAX ? INT32_MAX : r / gsize; };
     keys.push_back(Key{tail, grp(lo), grp(hi), lo, hi, (int32_t)i});
   }
   std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {

@@ -18,6 +18,7 @@ struct SchedParams {
   bool compress_cols = true;        // uint16 column offsets when the spans allow
   int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
   bool window = true;               // stage the short chunks' column window in LDS
+  int order_groups = 16;            // locality order: long-row rank groups (tpl_layout.h)
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
@@ -69,14 +70,14 @@ int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int reque
 // the order would not change (no long rows). Short rows first, keyed by the long
 // columns they reference — (tail, group(lo), group(hi), rank(lo), rank(hi), row) with
 // lo / hi the smallest / largest referenced long column, rank = its position among the
-// long rows, group = rank * kOrderGroups / n_long, and tail = 1 for rows that also
+// long rows, group = rank / ceil(n_long / G) (G = SchedParams::order_groups, 16 by
+// default; tpl_op_tune_order tries others), and tail = 1 for rows that also
 // reference another short row (they go last, next to the long columns, so the chunks
 // that hold them keep the narrow column spans of uint16 columns and the LDS window) —
 // then the long rows, ascending. For the
 // KKT matrices this orders the arcs by (endpoint group, endpoint group, endpoints):
 // the arcs of each node then lie in a few compact runs, so the long-row bins' gathers
 // of a node's arcs hit lines their neighbours have just fetched.
-constexpr int kOrderGroups = 16;
 std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
                                     const std::vector<int32_t>& col, const SchedParams& sp);
 // P A P^T in CSR: internal row i = the caller's row perm[i], columns mapped through

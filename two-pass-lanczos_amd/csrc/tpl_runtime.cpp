@@ -123,9 +123,10 @@ constexpr size_t kDevFtkMaxK = 1365;
 // (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
 // ~15-25 us (sync, host solve, upload, launch): one graph pays up to k ~ 128.
 constexpr size_t kDevFtkAutoK = 128;
-// Locality order, auto mode: on up to this many rows. Measured k_p2_spmv (KKT, D = 0):
-// 500k arcs 8.4 -> 7.0-7.6 us; 1M and 2M arcs within +-4 %; 5M arcs 54 -> 58 us
-// (the gathered vector, 40 MB, no longer fits the XCDs' L2s; profiles/r02_order_lab.txt).
+// Locality order, auto mode: on up to this many rows. Measured k_p2_spmv (KKT, D = 0;
+// profiles/r02_order_lab.txt): 500k arcs 8.76 -> 6.91 us, 1M arcs 12.8 -> 11.8 us,
+// 50k / 5k arcs flat; 2M arcs 20.5 -> 21.8 us and 5M arcs 54 -> 58 us (the gathered
+// vector, 16-40 MB, no longer fits the XCDs' L2s).
 constexpr int64_t kReorderAutoMaxRows = 1 << 20;
 }
 
@@ -1401,8 +1402,51 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
 
 
 // ------------------------------------------------------------ locality order
+tpl_status tpl_op_tune_order(tpl_op_t op, const int32_t* groups, int32_t count, int32_t iters,
+                             int32_t* chosen, double* best_us) {
+  return guarded([&] {
+    if (!op || count < 0 || (count > 0 && !groups) || iters <= 0)
+      fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
+    if (op->dist) fail(TPL_ERR_UNSUPPORTED, "the locality order is single-GPU only");
+    set_device(op);
+    sync_checked(op);
+    static const int32_t kDefault[] = {12, 13, 14, 15, 16, 17, 18, 19, 20, 22, 24};
+    const int32_t* list = count > 0 ? groups : kDefault;
+    const int32_t cnt = count > 0 ? count : (int32_t)(sizeof(kDefault) / sizeof(kDefault[0]));
+    for (int32_t i = 0; i < cnt; ++i)
+      if (list[i] <= 0) fail(TPL_ERR_INVALID_ARGUMENT, "group counts must be positive");
+    op->reorder = 1;
+    // any non-zero b: the timed SpMV launches need a step's valid partials and norms
+    const std::vector<double> ones(op->n, 1.0);
+    double best = 0.0;
+    int32_t best_g = op->sp.order_groups;
+    for (int32_t i = 0; i < cnt; ++i) {
+      op->sp.order_groups = list[i];
+      rebuild_schedule(op);
+      if (op->perm.empty()) break;  // no long rows: nothing to order
+      if (op->n > 0)
+        HIPCHK(hipMemcpy(op->b, ones.data(), op->n * sizeof(double), hipMemcpyHostToDevice));
+      double t1 = 0.0, t2 = 0.0;
+      for (const auto& kt : {std::make_pair(TPL_KERNEL_PASS1_SPMV, &t1),
+                             std::make_pair(TPL_KERNEL_PASS2_SPMV, &t2)}) {
+        const tpl_status st = tpl_profile_kernel(op, kt.first, iters, kt.second, nullptr);
+        if (st != TPL_OK) fail(st, tpl_last_error());
+      }
+      if (i == 0 || t1 + t2 < best) {
+        best = t1 + t2;
+        best_g = list[i];
+      }
+    }
+    op->sp.order_groups = best_g;
+    rebuild_schedule(op);
+    if (chosen) *chosen = best_g;
+    if (best_us) *best_us = best;
+  });
+}
+
 tpl_status tpl_locality_order(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
-                              int32_t short_row_max, int32_t* perm, int32_t* applied) {
+                              int32_t short_row_max, int32_t groups, int32_t* perm,
+                              int32_t* applied) {
   return guarded([&] {
     if (n < 0 || (n > 0 && (!row_ptr || !perm)) || !applied)
       fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
@@ -1413,6 +1457,7 @@ tpl_status tpl_locality_order(int64_t n, const int64_t* row_ptr, const int32_t* 
     std::vector<int32_t> col(col_idx, col_idx + (n > 0 ? row_ptr[n] : 0));
     SchedParams sp;
     sp.short_row_max = short_row_max > 0 ? short_row_max : -1;
+    if (groups > 0) sp.order_groups = groups;
     const std::vector<int32_t> p = locality_order(n, rp, col, sp);
     *applied = p.empty() ? 0 : 1;
     for (int64_t i = 0; i < n; ++i) perm[i] = p.empty() ? (int32_t)i : p[i];

@@ -118,8 +118,11 @@ tpl_op_set_device_ftk = _sig("tpl_op_set_device_ftk", c_int, c_void_p, c_int)
 tpl_op_device_bytes = _sig("tpl_op_device_bytes", c_int, c_void_p, POINTER(ctypes.c_uint64))
 tpl_op_set_reorder = _sig("tpl_op_set_reorder", c_int, c_void_p, c_int)
 tpl_op_permutation = _sig("tpl_op_permutation", c_int, c_void_p, POINTER(c_int32))
+tpl_op_tune_order = _sig("tpl_op_tune_order", c_int, c_void_p, POINTER(c_int32), c_int32,
+                         c_int32, POINTER(c_int32), POINTER(c_double))
 tpl_locality_order = _sig("tpl_locality_order", c_int, c_int64, POINTER(c_int64),
-                          POINTER(c_int32), c_int32, POINTER(c_int32), POINTER(c_int32))
+                          POINTER(c_int32), c_int32, c_int32, POINTER(c_int32),
+                          POINTER(c_int32))
 tpl_op_reorth_second_passes = _sig("tpl_op_reorth_second_passes", c_int, c_void_p, POINTER(c_int64))
 
 # built-in f(T_k) solvers: raw C function pointers usable as tpl_ftk_fn
@@ -144,7 +147,7 @@ EXPORTED = [
     "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_generate_kkt", "tpl_op_flags",
     "tpl_op_set_value_format", "tpl_op_set_device_ftk",
     "tpl_op_device_bytes", "tpl_op_reorth_second_passes", "tpl_op_set_reorder",
-    "tpl_op_permutation", "tpl_locality_order",
+    "tpl_op_permutation", "tpl_locality_order", "tpl_op_tune_order",
 ]
 
 

@@ -57,7 +57,7 @@ def _as_csr_arrays(a):
             m.data.astype(np.float64))
 
 
-def locality_order(a, short_row_max: int = -1):
+def locality_order(a, short_row_max: int = -1, groups: int = 16):
     """The device's locality row order for matrix ``a`` (tpl_locality_order; host only):
     perm[i] = the row held at internal position i, or None when it is the identity."""
     n, rp, ci, _ = _as_csr_arrays(a)
@@ -65,7 +65,8 @@ def locality_order(a, short_row_max: int = -1):
     applied = c_int32()
     check(_lib.tpl_locality_order(n, rp.ctypes.data_as(POINTER(c_int64)),
                                   ci.ctypes.data_as(POINTER(c_int32)), int(short_row_max),
-                                  perm.ctypes.data_as(POINTER(c_int32)), byref(applied)))
+                                  int(groups), perm.ctypes.data_as(POINTER(c_int32)),
+                                  byref(applied)))
     return perm[:n].copy() if applied.value else None
 
 
@@ -156,6 +157,15 @@ class HipCsrOp:
         return {"short_rows": sr[:ns.value].copy(), "long_rows": lr[:nl.value].copy(),
                 "G2": g2.value, "E": e.value, "slices": sl.value,
                 "perm": None if ident else perm.copy()}
+
+    def tune_order(self, groups=None, iters: int = 100):
+        """Time the pass-one and pass-two SpMV under each locality-order group count
+        (default 12..20, 22, 24) and keep the fastest: -> (groups, microseconds)."""
+        g = np.ascontiguousarray(groups if groups is not None else [], dtype=np.int32)
+        chosen, us = c_int32(), c_double()
+        check(_lib.tpl_op_tune_order(self._op, g.ctypes.data_as(POINTER(c_int32)) if g.size else None,
+                                     int(g.size), int(iters), byref(chosen), byref(us)))
+        return int(chosen.value), float(us.value)
 
     def set_reorder(self, mode=2):
         """Locality row order on the device (rebuilds the layout): False / 0 off,
