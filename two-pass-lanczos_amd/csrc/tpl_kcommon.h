@@ -122,6 +122,35 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
   return block_sum(s, red);
 }
 
+// The same canonical reduction computed by every wave on its own, for N <= 256 (one
+// partial per thread t of the tree): lane l holds s_t for the four threads t = l + 64u
+// (u = 0..3) of the four waves, four butterflies give the four wave totals, combined
+// as tree256 combines them — bit for bit the block result, without LDS or barriers (a
+// barrier in the middle of an SpMV waits for every wave's outstanding gathers).
+// wave_red selects the load pattern: lane-major for the wave reduction, else the
+// block pattern of load_partials (the choice is uniform per launch).
+template <int R>
+__device__ __forceinline__ void load_partials_sel(const double* __restrict__ P, int N,
+                                                  bool wave_red, PartialRegs<R>& r) {
+  const int l = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < R; ++u)
+    r.v[u] = P[clampi(wave_red ? l + 64 * u : (int)threadIdx.x + u * kTPB, N - 1)];
+}
+template <int R>
+__device__ __forceinline__ double finish_partials_wave(int N, const PartialRegs<R>& r) {
+  static_assert(R >= 4, "four sub-waves");
+  const int l = threadIdx.x & 63;
+  double t[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    double s = 0.0;
+    if (l + 64 * u < N) s = s + r.v[u];
+    t[u] = wave_sum(s);
+  }
+  return (t[0] + t[1]) + (t[2] + t[3]);
+}
+
 // Vector results of a step (w, v_{j+1}, x, r_{j+1}) are consumed only by the NEXT
 // launch. Stored write-through (agent-scope relaxed stores: global_store ... sc1) they
 // leave the XCD's L2 while the kernel runs, instead of as dirty lines written back at

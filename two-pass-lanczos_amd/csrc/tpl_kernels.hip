@@ -85,7 +85,12 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   asm volatile("" ::"s"(S.Pb_r), "s"(S.flags), "s"(S.norms), "s"(S.betas), "s"(S.Pa), "s"(A.G2_r),
                "s"(xsrc), "s"(r_cur), "s"(r_prev), "s"(W), "s"(Vcol), "s"(j));
   PartialRegs<4> pr;           // G2 <= 1024
-  load_partials(S.Pb_r, A.G2_r, pr);
+  const bool wave_red = A.G2_r <= kTPB;  // beta reduced by each wave alone (no barrier)
+  load_partials_sel(S.Pb_r, A.G2_r, wave_red, pr);
+  // the stop flag and beta_{j-2} with the partials, ahead of the entries and gathers:
+  // read later, their wait would drain every gather in flight before the beta chain
+  const int stop0 = S.flags[0];
+  const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
   EpiPass1 epi;
   epi.r_cur = r_cur;
   epi.r_prev = (j >= 2) ? r_prev : r_cur;
@@ -97,13 +102,13 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   epi.Vcol = Vcol;
   epi.Pa_long = S.Pa + A.n_chunks;
   // beta_{j-1} (||b|| at j = 1) from the norm partials; fills the epilogue. Runs once the
-  // workgroup's loads are in flight: the stop flag and beta_{j-2} (DevState scalars)
-  // are waited on only here.
+  // workgroup's loads are in flight.
   auto scale_fn = [&]() -> Scale {
     __builtin_amdgcn_sched_barrier(0);
-    if (S.flags[0]) return Scale{0.0, false};
-    epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
-    const double beta = sqrt(finish_partials(S.Pb_r, A.G2_r, pr, red));
+    if (stop0) return Scale{0.0, false};
+    epi.invN_prev = (j >= 2) ? 1.0 / norm_prev : 0.0;
+    const double beta = sqrt(wave_red ? finish_partials_wave(A.G2_r, pr)
+                                      : finish_partials(S.Pb_r, A.G2_r, pr, red));
     if (beta <= kBreakdownTol) {
       // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
       // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed
