@@ -214,7 +214,7 @@ struct EpiPass1 {
   double* Pa_long;      // alpha partials of the long rows (Pa + n_chunks)
   __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
   // long row r: its alpha partial is the single rounded product v * w
-  __device__ __forceinline__ void long_alpha(int r, double acc) const { Pa_long[r] = acc; }
+  __device__ __forceinline__ void long_alpha(int r, double acc) const { st_out(Pa_long + r, acc); }
   // returns v_j[i]
   __device__ __forceinline__ double apply(int i, double s, const Pre1& p, double& acc) const {
     const double v = p.rc * invN_cur;

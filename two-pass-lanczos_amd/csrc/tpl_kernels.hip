@@ -131,7 +131,9 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   const int slot = spmv_block<F>(A, xsrc, scale_fn, epi, acc, lds);
   if (slot < 0) return; // uniform per workgroup
   const double p = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pa[slot] = p;
+  // write-through: every k_p1_axpy workgroup, on every XCD, reads all the partials
+  // next (measured: pass one -0.2 to -0.3 us per step against a plain store)
+  if (threadIdx.x == 0) st_out(S.Pa + slot, p);
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
@@ -209,7 +211,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     step(i0, *reinterpret_cast<const double2*>(W + i0),
          *reinterpret_cast<const double2*>(r_cur + i0));
   const double p = block_sum(acc, red);
-  if (threadIdx.x == 0) S.Pb[rb] = p;
+  if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
 }
 
 // Pass two prologue: v_1 = b * (1/||b||); x = v_1 * y_1 (src/algorithms/lanczos_two_pass.rs:248-252).
