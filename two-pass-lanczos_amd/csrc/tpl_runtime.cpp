@@ -196,6 +196,7 @@ struct tpl_op_s {
   // cross the boundary through a gather (internal i <- caller's perm[i], back via iperm).
   // h_rowptr / h_col / h_val keep the caller's order.
   int reorder = 2;                  // 0 off, 1 on, 2 auto (n <= kReorderAutoMaxRows)
+  bool local_order = false;         // replicated partition: own short rows in locality order
   std::vector<int32_t> perm, iperm;
   int32_t* d_perm = nullptr;
   int32_t* d_iperm = nullptr;
@@ -308,7 +309,7 @@ void rebuild_schedule(tpl_op_s* op) {
   // few lines and the LDS window costs more than it saves (measured +0.4 us per SpMV at
   // 500k): window only in the caller's order.
   SchedParams sp = op->sp;
-  sp.window = !p;
+  sp.window = !p && !op->local_order;
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
@@ -945,7 +946,7 @@ int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
   return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0) |
          (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0) | (op->last_one_graph ? 32 : 0) |
-         (op->d_perm ? 64 : 0);
+         (op->d_perm || op->local_order ? 64 : 0);
 }
 
 tpl_status tpl_op_set_reorder(tpl_op_t op, int mode) {
@@ -1646,11 +1647,49 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
     const int64_t ns = cut[me + 1] - cut[me], nl = (int64_t)Lr.size();
     op->ns_local = ns;
     op->n = ns + nl;
+    // this rank's short rows; in the locality order (tpl_layout.h locality_order, the
+    // same key over the replicated long rows' ranks) when the rank's rows fit the auto
+    // rule. The local order is the caller's to follow through tpl_op_local_rows, so no
+    // vector is permuted on the device.
+    std::vector<int64_t> mine(S.begin() + cut[me], S.begin() + cut[me + 1]);
+    if (nl > 0 && op->n <= kReorderAutoMaxRows) {
+      const int32_t gsize = (int32_t)((nl + 15) / 16);
+      struct Key {
+        int32_t tail, glo, ghi, rlo, rhi;
+        int64_t row;
+      };
+      std::vector<Key> keys;
+      keys.reserve(mine.size());
+      for (int64_t i : mine) {
+        int32_t lo = INT32_MAX, hi = INT32_MAX, tail = 0;
+        for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+          const int32_t r = lidx[col_idx[q]];
+          if (r < 0) {
+            tail |= col_idx[q] != i;
+            continue;
+          }
+          if (lo == INT32_MAX) lo = r;
+          hi = r;
+        }
+        auto grp = [&](int32_t r) { return r == INT32_MAX ? INT32_MAX : r / gsize; };
+        keys.push_back(Key{tail, grp(lo), grp(hi), lo, hi, i});
+      }
+      std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+        if (x.tail != y.tail) return x.tail < y.tail;
+        if (x.glo != y.glo) return x.glo < y.glo;
+        if (x.ghi != y.ghi) return x.ghi < y.ghi;
+        if (x.rlo != y.rlo) return x.rlo < y.rlo;
+        if (x.rhi != y.rhi) return x.rhi < y.rhi;
+        return x.row < y.row;
+      });
+      for (size_t p = 0; p < keys.size(); ++p) mine[p] = keys[p].row;
+      op->local_order = true;
+    }
     op->g2l.assign(n, -1);
     op->local_rows.resize(op->n);
     for (int64_t p = 0; p < ns; ++p) {
-      op->g2l[S[cut[me] + p]] = (int32_t)p;
-      op->local_rows[p] = S[cut[me] + p];
+      op->g2l[mine[p]] = (int32_t)p;
+      op->local_rows[p] = mine[p];
     }
     for (int64_t l = 0; l < nl; ++l) {
       op->g2l[Lr[l]] = (int32_t)(ns + l);
