@@ -268,6 +268,8 @@ def main():
                                + ("" if not partitioned else f", rows partitioned over {world} GPUs"),
                    "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
                    "graphs": op.uses_graphs,
+                   # tpl_op_flags bit 6: the device holds the rows in the locality order
+                   "row_order": "locality" if op.flags() & 64 else "caller",
                    "parallelism": "single" if not partitioned
                    else (f"{op.mode}{world} (" + ("long-row partials all-gathered per SpMV"
                          if op.mode == "replicated" else "vector all-gathered per SpMV")
