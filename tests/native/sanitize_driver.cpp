@@ -201,6 +201,38 @@ static void layout_checks() {
     CHECK(seen_short == want_short && seen_long == want_long, "entries n=%lld: short %lld/%lld long %lld/%lld",
           (long long)c.n, (long long)seen_short, (long long)want_short, (long long)seen_long,
           (long long)want_long);
+    // the locality order (a permutation, long rows last) and P A P^T (same entries,
+    // columns ascending), then the layout of P A P^T
+    for (int groups : {1, 16, 1000}) {
+      tpl::SchedParams so = sp;
+      so.order_groups = groups;
+      const std::vector<int32_t> perm = tpl::locality_order(c.n, rp, col, so);
+      if (perm.empty()) continue;
+      std::vector<int32_t> iperm(c.n, -1);
+      bool is_perm = (int64_t)perm.size() == c.n;
+      for (int64_t i = 0; is_perm && i < c.n; ++i) {
+        is_perm = perm[i] >= 0 && perm[i] < c.n && iperm[perm[i]] < 0;
+        if (is_perm) iperm[perm[i]] = (int32_t)i;
+      }
+      CHECK(is_perm, "locality order n=%lld is not a permutation", (long long)c.n);
+      if (!is_perm) continue;
+      std::vector<int32_t> prp, pcol;
+      std::vector<double> pval;
+      tpl::permute_csr(c.n, rp, col, val, perm, iperm, prp, pcol, pval);
+      bool ok = prp.size() == rp.size() && pcol.size() == col.size();
+      for (int64_t i = 0; ok && i < c.n; ++i) {
+        const int32_t e = perm[i];
+        ok = prp[i + 1] - prp[i] == rp[e + 1] - rp[e];
+        for (int32_t q = prp[i] + 1; ok && q < prp[i + 1]; ++q) ok = pcol[q] > pcol[q - 1];
+      }
+      CHECK(ok, "permuted CSR n=%lld", (long long)c.n);
+      try {
+        (void)tpl::build_layout(c.n, c.n, prp, pcol, pval, sp, tpl::ColMap{});
+      } catch (const tpl::Error& e) {
+        std::printf("FAIL permuted layout n=%lld: %s\n", (long long)c.n, e.msg.c_str());
+        ++g_fail;
+      }
+    }
   }
 }
 
