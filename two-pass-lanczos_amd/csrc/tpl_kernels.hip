@@ -89,8 +89,11 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   load_partials_sel(S.Pb_r, A.G2_r, wave_red, pr);
   // the stop flag and beta_{j-2} with the partials, ahead of the entries and gathers:
   // read later, their wait would drain every gather in flight before the beta chain
-  const int stop0 = S.flags[0];
-  const double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
+  int stop0 = S.flags[0];
+  double norm_prev = (j >= 2) ? S.norms[j - 2] : 1.0;
+  // keep these loads first: sunk below the gathers by the scheduler, their wait would
+  // again drain every gather before the beta chain
+  __builtin_amdgcn_sched_barrier(0);
   EpiPass1 epi;
   epi.r_cur = r_cur;
   epi.r_prev = (j >= 2) ? r_prev : r_cur;
@@ -105,6 +108,9 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   // workgroup's loads are in flight.
   auto scale_fn = [&]() -> Scale {
     __builtin_amdgcn_sched_barrier(0);
+    // opaque here: the optimiser would otherwise hoist the stop test and the reciprocal
+    // to the loads, making every workgroup wait for them before issuing its entries
+    asm volatile("" : "+v"(stop0), "+v"(norm_prev));
     if (stop0) return Scale{0.0, false};
     epi.invN_prev = (j >= 2) ? 1.0 / norm_prev : 0.0;
     const double beta = sqrt(wave_red ? finish_partials_wave(A.G2_r, pr)
