@@ -19,15 +19,25 @@ namespace tpl {
 // recent SpMV-shaped launch — [0] start, [1] scale known, [2] products staged /
 // row sums done, [3] piece sums staged, [4] publish drained, [5] end — read back
 // by tpl_debug_stamps().
-constexpr int kMarks = 6;
+constexpr int kMarks = 7;  // marks 0..5 + the workgroup's HW_ID / XCC_ID in slot 6
 __device__ unsigned long long g_stamps[kMarks * 65536];
 #define TPL_MARK(k)                                                          \
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < 65536)                              \
       g_stamps[kMarks * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+#define TPL_MARK_ID()                                                        \
+  do {                                                                       \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) {                            \
+      unsigned hw_, xcc_;                                                    \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));     \
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_)); \
+      g_stamps[kMarks * blockIdx.x + 6] = ((unsigned long long)xcc_ << 32) | hw_; \
+    }                                                                        \
+  } while (0)
 #else
 #define TPL_MARK(k) do {} while (0)
+#define TPL_MARK_ID() do {} while (0)
 #endif
 
 // ---------------------------------------------------------------- reductions
@@ -716,6 +726,7 @@ __device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restr
                                           double* lds) {
 #if TPL_STAMP
   TPL_MARK(0);
+  TPL_MARK_ID();
   const int r = spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
   TPL_MARK(5);
   return r;
