@@ -128,7 +128,17 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
 #pragma unroll
   for (int u = 0; u < R; ++u)
     if ((int)threadIdx.x + u * kTPB < N) s = s + r.v[u];
-  for (int i = threadIdx.x + R * kTPB; i < N; i += kTPB) s = s + P[i]; // N > 256 R (rare)
+  // N > 256 R (the 5M-arc instance: ~13k alpha partials): the rest in batches of 8
+  // loads in flight, added in the same ascending order (a plain loop waits for each
+  // load before the next is issued: one round trip per 256 partials)
+  for (int i0 = threadIdx.x + R * kTPB; i0 - (int)threadIdx.x < N; i0 += 8 * kTPB) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = P[clampi(i0 + u * kTPB, N - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (i0 + u * kTPB < N) s = s + t[u];
+  }
   return block_sum(s, red);
 }
 
