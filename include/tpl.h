@@ -331,12 +331,18 @@ enum {
   TPL_KERNEL_PASS1_SPMV = 0, /* pass one: SpMV + beta-AXPY + alpha partials             */
   TPL_KERNEL_PASS1_AXPY = 1, /* pass one: alpha-AXPY + ||w||^2 partials                 */
   TPL_KERNEL_PASS2_SPMV = 2, /* pass two: SpMV + both AXPYs + scale + x += y v          */
-  TPL_KERNEL_SPMV = 3        /* plain y = A x                                           */
+  TPL_KERNEL_SPMV = 3,       /* plain y = A x                                           */
+  /* partitioned operators only (SURVEY.md §8(e) "comm fraction"): the exchanges one
+   * step issues, exactly as the pass graphs issue them (rank totals + all-gathers)  */
+  TPL_KERNEL_EXCHANGE_P1 = 4, /* a pass-one step's exchanges                           */
+  TPL_KERNEL_EXCHANGE_P2 = 5  /* a pass-two step's exchange                            */
 };
 /* Time `iters` back-to-back launches of one kernel on the operator's stream with
  * HIP events (a warm-up launch first). Returns the average per launch in
  * microseconds (event-to-event, so it includes the launch gap) and the
- * algorithmic bytes one launch moves ("Algorithmic bytes").          */
+ * algorithmic bytes one launch moves ("Algorithmic bytes"). The
+ * exchange ids are collective: every rank calls with the same arguments; their
+ * bytes are those one rank receives.                                            */
 tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us,
                               double* algo_bytes);
 /* Algorithmic bytes of one launch of `kernel` (no GPU work). */

@@ -34,7 +34,11 @@ def main():
     xs = tpl_amd.lanczos(op, bl, k, "inv")
     y = op.apply(op.local(np.cos(np.arange(a.shape[0]))))
     sch = op.schedule()  # this rank's layout: the partition oracle's reduction order
-    np.savez(os.path.join(out, f"rank{rank}.npz"), x1=x1, x2=x2, xs=xs, y=y,
+    # the exchange timing ids (collective; bench.py's comm fraction), then a solve again:
+    # profiling leaves nothing behind that changes the next solve
+    ex = [op.profile_kernel(k_id, 5) for k_id in (4, 5)]
+    x3 = tpl_amd.lanczos_two_pass(op, bl, k, "inv")
+    np.savez(os.path.join(out, f"rank{rank}.npz"), x1=x1, x2=x2, x3=x3, ex_us=[e[0] for e in ex], ex_bytes=[e[1] for e in ex], xs=xs, y=y,
              al=dec.alphas, be=dec.betas, steps=dec.steps_taken, bn=dec.b_norm,
              rows=op.local_rows, mode=op.mode, s_short=sch["short_rows"],
              s_long=sch["long_rows"], s_G2=sch["G2"], s_E=sch["E"], s_slices=sch["slices"],

@@ -64,15 +64,30 @@ def test_one_rank_rccl_rows_bitwise(kkt_tmp, tmp_path):
     a, x, dec, xs = _single(kkt_tmp)  # same layout as the partition's
     r = _run_ranks(str(tmp_path), 1, "rccl", mode="rows")[0]
     assert str(r["mode"]) == "rows"
+    _check_exchange_profile([r])
     assert np.array_equal(r["x1"], x)
     assert np.array_equal(r["al"], dec.alphas) and np.array_equal(r["be"], dec.betas)
     assert np.array_equal(r["xs"], xs)
+
+
+def _check_exchange_profile(rs):
+    # tpl_profile_kernel's exchange ids: positive times, the bytes one rank receives
+    # (pass one: the alpha and beta totals + one vector part per rank; pass two: the part)
+    R = len(rs)
+    for r in rs:
+        assert np.array_equal(r["x3"], r["x1"])
+        assert all(t > 0 for t in r["ex_us"])
+        b1, b2 = r["ex_bytes"]
+        assert b1 - b2 == 16 * R and b2 > 0
+        if str(r["mode"]) == "replicated":
+            assert b2 == 8 * R * len(r["s_long"])
 
 
 def test_one_rank_rccl_replicated(kkt_tmp, tmp_path):
     a, x, dec, xs = _single(kkt_tmp)
     r = _run_ranks(str(tmp_path), 1, "rccl", mode="replicated")[0]
     assert str(r["mode"]) == "replicated"
+    _check_exchange_profile([r])
     xr = _assemble([r], "x1", a.shape[0])
     assert np.linalg.norm(xr - x) <= 1e-10 * np.linalg.norm(x)
     _check_partition_order(a, [r], "replicated", 50)
@@ -106,6 +121,7 @@ def test_ranks_share_gpu_host_transport(kkt_tmp, tmp_path, world, mode):
     n = a.shape[0]
     xd = _assemble(rs, "x1", n)
     assert np.array_equal(xd, _assemble(rs, "x2", n))  # deterministic
+    _check_exchange_profile(rs)
     assert np.linalg.norm(xd - x) <= 1e-10 * np.linalg.norm(x)
     xsd = _assemble(rs, "xs", n)
     assert np.linalg.norm(xsd - xs) <= 1e-10 * np.linalg.norm(xs)

@@ -534,37 +534,29 @@ void enqueue_p1_prologue(tpl_op_s* op) {
   }
 }
 
-// Pass one, step j (k = requested steps).
-void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
-  const CsrDev A = csr_dev(op);
-  HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
-                         op->W, Vcol, j, op->stream));
+// The exchanges of a pass-one step of a partitioned operator: (a) after the SpMV launch
+// (the alpha total; with replicated long rows their partials travel with it), (b) after
+// the AXPY (the beta total; with row blocks r_{j+1} travels with it).
+void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
   if (op->hybrid) {
     // short-row alpha total and the long rows' partials travel together; every rank then
     // finishes the long rows itself (replicated) and adds their alpha once
-    const int R = op->dist->nranks;
     const size_t nl = op->lay.lrows.size();
     dist_total(op, op->S.Pa, A.n_chunks, op->d_rsum + op->dist->rank);
     dist_group(op, true);
     dist_allgather(op, op->d_rsum, 1);
     if (nl) dist_allgather(op, op->d_yall, nl);
     dist_group(op, false);
-    HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, R, r_of(op, j),
-                               j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol, op->d_rsum + R, j,
-                               op->stream));
-    HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
-    if (j < k) {
-      dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
-      dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
-    }
-    return;
-  }
-  if (op->dist) {
+  } else {
     dist_total(op, op->S.Pa, A.NA, op->d_rsum + op->dist->rank);
     dist_allgather(op, op->d_rsum, 1);
   }
-  HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
-  if (op->dist && j < k) {
+}
+void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
+  if (op->hybrid) {
+    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+    dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+  } else {
     const int R = op->dist->nranks;
     dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
     dist_group(op, true);
@@ -572,6 +564,29 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
     dist_allgather(op, op->RG[(j + 1) % 3], (size_t)op->ld);
     dist_group(op, false);
   }
+}
+// The exchange after pass-two step j's SpMV launch.
+void enqueue_p2_exchange(tpl_op_s* op, int j) {
+  if (op->hybrid) {
+    const size_t nl = op->lay.lrows.size();
+    if (nl) dist_allgather(op, op->d_yall, nl);
+  } else {
+    dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
+  }
+}
+
+// Pass one, step j (k = requested steps).
+void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
+  const CsrDev A = csr_dev(op);
+  HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
+                         op->W, Vcol, j, op->stream));
+  if (op->dist) enqueue_p1_exchange_a(op, A);
+  if (op->hybrid)
+    HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, op->dist->nranks, r_of(op, j),
+                               j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol,
+                               op->d_rsum + op->dist->nranks, j, op->stream));
+  HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
+  if (op->dist && j < k) enqueue_p1_exchange_b(op, A, j);
 }
 
 void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth) {
@@ -596,13 +611,12 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
                            Vcol, j, nflush, 0, op->stream));
     if (op->hybrid) {
-      const size_t nl = op->lay.lrows.size();
-      if (nl) dist_allgather(op, op->d_yall, nl);
+      enqueue_p2_exchange(op, j);
       HIPCHK(launch::long_epi_p2(A, op->S, op->d_yall, op->dist->nranks, op->V2[j % 3],
                                  j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3],
                                  op->x, Vcol, j, nflush, op->stream));
     } else if (op->dist && j + 1 < (int)steps) {
-      dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
+      enqueue_p2_exchange(op, j);
     }
   }
 }
@@ -1286,6 +1300,15 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
     case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;         // w, r_j read; r_{j+1} written
     // + v_{j-1} read; x read and written once per three steps (grouped x updates)
     case TPL_KERNEL_PASS2_SPMV: return spmv + 8.0 * n + 16.0 * n / 3.0;
+    case TPL_KERNEL_EXCHANGE_P1:
+    case TPL_KERNEL_EXCHANGE_P2: {
+      if (!op->dist) return 0.0;
+      const double R = (double)op->dist->nranks;
+      const double vec = op->hybrid ? (double)op->lay.lrows.size() : (double)op->ld;
+      // pass one: the alpha and beta totals and one vector part per rank; pass two: the
+      // vector part only (the row-block pass two gathers v, no totals)
+      return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (vec + 2.0) : 8.0 * R * vec;
+    }
     default: return 0.0;
   }
 }
@@ -1367,9 +1390,18 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
                                  op->V2[(i + 1) % 3], op->V2[i % 3], op->x, nullptr, 2,
                                  i % 3 == 2 ? 3 : 0, 0, op->stream));
           break;
+        case TPL_KERNEL_EXCHANGE_P1:
+          enqueue_p1_exchange_a(op, A);
+          enqueue_p1_exchange_b(op, A, 2);
+          break;
+        case TPL_KERNEL_EXCHANGE_P2:
+          enqueue_p2_exchange(op, 2 + i);
+          break;
         default: fail(TPL_ERR_INVALID_ARGUMENT, "unknown kernel id");
       }
     };
+    const bool exchange = kernel == TPL_KERNEL_EXCHANGE_P1 || kernel == TPL_KERNEL_EXCHANGE_P2;
+    if (exchange && !op->dist) fail(TPL_ERR_INVALID_ARGUMENT, "exchange ids need a partitioned operator");
     // Valid state for repeated launches: flags clear, partials/norms of a real step.
     HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
     HIPCHK(launch::p1_spmv(A, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
@@ -1379,6 +1411,20 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     HIPCHK(hipMemcpyAsync(op->V2[2], op->R[2], op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));
     sync_checked(op);
+    if (exchange && !op->dist->comm) {
+      // host transport (tests): its exchanges synchronise the stream, so no graph
+      launch_one(0);
+      sync_checked(op);
+      HIPCHK(hipEventRecord(op->ev0, op->stream));
+      for (int i = 0; i < iters; ++i) launch_one(i);
+      HIPCHK(hipEventRecord(op->ev1, op->stream));
+      HIPCHK(hipEventSynchronize(op->ev1));
+      float ms = 0.f;
+      HIPCHK(hipEventElapsedTime(&ms, op->ev0, op->ev1));
+      *avg_us = 1000.0 * (double)ms / iters;
+      if (algo_bytes) *algo_bytes = tpl_kernel_algo_bytes(op, kernel);
+      return;
+    }
     // The launches are captured into one graph, as the solver runs them: back-to-back
     // hipLaunchKernel calls would time the host's submission rate for short kernels.
     hipGraph_t g = nullptr;

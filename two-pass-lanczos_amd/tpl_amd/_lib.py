@@ -53,6 +53,8 @@ TPL_KERNEL_PASS1_SPMV = 0
 TPL_KERNEL_PASS1_AXPY = 1
 TPL_KERNEL_PASS2_SPMV = 2
 TPL_KERNEL_SPMV = 3
+TPL_KERNEL_EXCHANGE_P1 = 4
+TPL_KERNEL_EXCHANGE_P2 = 5
 
 PD = POINTER(c_double)
 
