@@ -297,14 +297,17 @@ def main():
         # SURVEY.md §8(e) "comm fraction": the exchanges of one pass-one / pass-two step
         # (rank totals + all-gathers, as the pass graphs issue them) timed alone, every
         # rank together; times the steps of one solve over the solve time (rank 0)
-        ex1 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P1, args.profile_iters)
-        ex2 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P2, args.profile_iters)
-        comm_ms = (steps_taken * ex1[0] + (steps_taken - 1) * ex2[0]) / 1000.0
-        out["exchange"] = {"pass1_us_per_step": round(ex1[0], 3),
-                           "pass2_us_per_step": round(ex2[0], 3),
-                           "bytes_received_per_step": [int(ex1[1]), int(ex2[1])],
-                           "ms_per_solve": round(comm_ms, 3),
-                           "comm_frac": round(comm_ms / (1000.0 * solve_s), 4)}
+        try:  # a diagnostic: its failure must not cost the measured line
+            ex1 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P1, args.profile_iters)
+            ex2 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P2, args.profile_iters)
+            comm_ms = (steps_taken * ex1[0] + (steps_taken - 1) * ex2[0]) / 1000.0
+            out["exchange"] = {"pass1_us_per_step": round(ex1[0], 3),
+                               "pass2_us_per_step": round(ex2[0], 3),
+                               "bytes_received_per_step": [int(ex1[1]), int(ex2[1])],
+                               "ms_per_solve": round(comm_ms, 3),
+                               "comm_frac": round(comm_ms / (1000.0 * solve_s), 4)}
+        except Exception as e:  # noqa: BLE001
+            out["exchange"] = {"error": str(e)}
     if args.pcie and not partitioned and world == 1:
         # PCIe-inclusive rate (never `value`): host b in, host x out, one H2D + one D2H
         xh = np.empty(n)

@@ -1411,8 +1411,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     HIPCHK(hipMemcpyAsync(op->V2[2], op->R[2], op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));
     sync_checked(op);
-    if (exchange && !op->dist->comm) {
-      // host transport (tests): its exchanges synchronise the stream, so no graph
+    auto time_eager = [&] {
       launch_one(0);
       sync_checked(op);
       HIPCHK(hipEventRecord(op->ev0, op->stream));
@@ -1423,6 +1422,12 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
       HIPCHK(hipEventElapsedTime(&ms, op->ev0, op->ev1));
       *avg_us = 1000.0 * (double)ms / iters;
       if (algo_bytes) *algo_bytes = tpl_kernel_algo_bytes(op, kernel);
+    };
+    // exchanges run as the solver runs them: eagerly when the transport cannot be
+    // captured (the host transport synchronises the stream; an RCCL that refused capture
+    // already switched the operator to eager launches, run_graph)
+    if (exchange && (!op->dist->comm || op->eager || !use_graphs())) {
+      time_eager();
       return;
     }
     // The launches are captured into one graph, as the solver runs them: back-to-back
@@ -1430,7 +1435,17 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     HIPCHK(hipStreamBeginCapture(op->stream, hipStreamCaptureModeThreadLocal));
-    for (int i = 0; i < iters; ++i) launch_one(i);
+    try {
+      for (int i = 0; i < iters; ++i) launch_one(i);
+    } catch (...) {
+      hipStreamEndCapture(op->stream, &g);
+      if (g) hipGraphDestroy(g);
+      if (!exchange) throw;
+      op->eager = true;  // as run_graph: the transport refused capture
+      hipGetLastError();
+      time_eager();
+      return;
+    }
     HIPCHK(hipStreamEndCapture(op->stream, &g));
     HIPCHK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
     hipGraphDestroy(g);
