@@ -39,6 +39,17 @@ def test_library_exports_every_header_symbol():
         assert re.search(rf"\bT {s}\b", nm), s
 
 
+def test_header_constants_match_python_mirror():
+    """Every TPL_KERNEL_* / TPL_MEM_* enumerator of the header has the same value in
+    the ctypes mirror (tpl_amd._lib), so the Python side passes what the ABI means."""
+    txt = open(os.path.join(ROOT, "include", "tpl.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    consts = dict(re.findall(r"\b(TPL_(?:KERNEL|MEM)_[A-Z0-9_]+)\s*=\s*(\d+)", txt))
+    assert {"TPL_KERNEL_EXCHANGE_P1", "TPL_KERNEL_EXCHANGE_P2"} <= set(consts)
+    for name, v in consts.items():
+        assert getattr(_lib, name) == int(v), name
+
+
 def test_library_is_gfx950_code_object():
     """The fat binary embeds an amdgcn code object for gfx950 (and nothing else)."""
     blob = open(_lib.LIB_PATH, "rb").read()
