@@ -105,6 +105,16 @@ __device__ __forceinline__ double block_sum(double v, double* red) {
   return r;
 }
 
+// block_sum for a kernel's last reduction, whose total only thread 0 stores: the same
+// bits, without the trailing barrier (red is not reused), so waves 1-3 retire at once.
+__device__ __forceinline__ double block_sum_tail(double v, double* red) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+
 // Issue the partial loads (independent) early ...
 template <int R>
 struct PartialRegs {

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
       acc = i0 < A.norm_n ? fma(v, v, acc) : acc;
     }
   }
-  const double p = block_sum(acc, red);
+  const double p = block_sum_tail(acc, red);
   if (threadIdx.x == 0) S.Pb[rb] = p;
 }
 
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   double acc = 0.0;
   const int slot = spmv_block<F>(A, xsrc, scale_fn, epi, acc, lds);
   if (slot < 0) return; // uniform per workgroup
-  const double p = block_sum(acc, red);
+  const double p = block_sum_tail(acc, red);
   // write-through: every k_p1_axpy workgroup, on every XCD, reads all the partials
   // next (measured: pass one -0.2 to -0.3 us per step against a plain store)
   if (threadIdx.x == 0) st_out(S.Pa + slot, p);
@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   for (int64_t i0 = i00 + (int64_t)kAxPairs * 2 * kTPB; i0 < end; i0 += 2 * kTPB) // E > 2048
     step(i0, *reinterpret_cast<const double2*>(W + i0),
          *reinterpret_cast<const double2*>(r_cur + i0));
-  const double p = block_sum(acc, red);
+  const double p = block_sum_tail(acc, red);
   if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
 }
 
@@ -425,7 +425,7 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
   epi.Vcol = Vcol;
   epi.Pa_long = nullptr;
   const double acc = long_epi_rows(A, yall, R, epi);
-  const double p = block_sum(acc, red);
+  const double p = block_sum_tail(acc, red);
   if (threadIdx.x == 0) Pa_long[blockIdx.x] = p;
 }
 
