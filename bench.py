@@ -63,6 +63,10 @@ def parse(argv=None):
     p.add_argument("--cpu-baseline", type=int, default=1, help="0 to skip the CPU leg")
     p.add_argument("--cpu-k", type=int, default=500, help="k of the bounded CPU sample")
     p.add_argument("--cpu-reps", type=int, default=2, help="CPU sample repetitions")
+    p.add_argument("--tune-order", type=int, default=1,
+                   help="1 (default): tpl_op_tune_order before the warm-up (setup-time autotune "
+                        "of the locality order's group count on this GPU, outside the timed "
+                        "region); 0: the untuned default order")
     p.add_argument("--profile-iters", type=int, default=200)
     p.add_argument("--other-configs", type=int, default=1,
                    help="N=1: also time BASELINE configs[0] and [1] (5k inv k=50, 50k exp k=200)")
@@ -161,9 +165,12 @@ def main():
     b = a @ np.full(n, 1.0 / np.sqrt(n))  # src/bin/tradeoff.rs:235-236
 
     dctx = None
+    tuned = None
     if not partitioned:
         op = tpl_amd.HipCsrOp(a, device=device)
         b_loc = b
+        if args.tune_order and op.flags() & 64:
+            tuned = op.tune_order()
     else:
         # row-partitioned operator: RCCL exchanges over xGMI
         if dist is None:
@@ -270,6 +277,8 @@ def main():
                    "graphs": op.uses_graphs,
                    # tpl_op_flags bit 6: the device holds the rows in the locality order
                    "row_order": "locality" if op.flags() & 64 else "caller",
+                   **({} if tuned is None else
+                      {"order_tuned": {"groups": tuned[0], "best_us": round(tuned[1], 3)}}),
                    "parallelism": "single" if not partitioned
                    else (f"{op.mode}{world} (" + ("long-row partials all-gathered per SpMV"
                          if op.mode == "replicated" else "vector all-gathered per SpMV")
