@@ -170,7 +170,10 @@ def main():
         op = tpl_amd.HipCsrOp(a, device=device)
         b_loc = b
         if args.tune_order and op.flags() & 64:
-            tuned = op.tune_order()
+            # 30 launches per candidate: enough to separate the group counts (0.2-0.8 us
+            # apart), few enough that a rocprofv3 run of this command stays dominated by
+            # the solves' launches
+            tuned = op.tune_order(iters=30)
     else:
         # row-partitioned operator: RCCL exchanges over xGMI
         if dist is None:
