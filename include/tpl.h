@@ -56,6 +56,28 @@ typedef struct tpl_op_s* tpl_op_t;   /* device-resident CSR operator A    */
 
 /* Thread-local message of the last failing call ("" after success). */
 const char* tpl_last_error(void);
+/* The fields of the last failing call's LanczosErrorKind (src/error.rs:20-58), so a
+ * binding rebuilds the variant itself instead of parsing the message:
+ *   TPL_ERR_INPUT              InputError(inner)
+ *   TPL_ERR_PARAMETER_MISMATCH ParameterMismatch { param_name, expected, actual }
+ *                              (src/solvers.rs:78-85,158-165; lanczos_two_pass.rs:220-227)
+ *   TPL_ERR_DIMENSION_MISMATCH DimensionMismatch { operator_cols, vector_rows }
+ *   TPL_ERR_SOLVER             SolverError(inner) (src/solvers.rs:75,156)
+ *   TPL_ERR_EVD                EvdError(inner)
+ *   TPL_ERR_BREAKDOWN          Breakdown { k = breakdown_step } (never raised: a
+ *                              breakdown truncates steps_taken, as in the reference)
+ * status is TPL_OK after a successful call. The strings stay valid until the next
+ * tpl_* call on this thread. Returns TPL_ERR_INVALID_ARGUMENT only for out == NULL.  */
+typedef struct tpl_error_detail {
+  int32_t status;             /* tpl_status of the last call on this thread            */
+  const char* message;        /* == tpl_last_error(): the variant's Display text        */
+  const char* inner;          /* InputError / SolverError / EvdError payload, else ""  */
+  const char* param_name;     /* ParameterMismatch::param_name, else ""                */
+  uint64_t expected, actual;  /* ParameterMismatch                                      */
+  uint64_t operator_cols, vector_rows; /* DimensionMismatch                             */
+  uint64_t breakdown_step;    /* Breakdown::k                                           */
+} tpl_error_detail;
+tpl_status tpl_last_error_detail(tpl_error_detail* out);
 /* Library version string, e.g. "tpl_amd 0.1.0 gfx950". */
 const char* tpl_version(void);
 
@@ -85,7 +107,9 @@ int64_t tpl_op_nnz(tpl_op_t op);
  * as int8, bit 3 / bit 4: short-row / long-row column indices kept as uint16 offsets
  * (see tpl_op_set_value_format), bit 5: the last tpl_lanczos_two_pass ran as one
  * device graph (device f(T_k)), bit 6: rows held in the locality order
- * (tpl_op_set_reorder). -1 if op is NULL.                                          */
+ * (tpl_op_set_reorder, tpl_op_permutation; on a replicated-long-row partition the
+ * rank's own short rows are in that order and tpl_op_local_rows, not
+ * tpl_op_permutation, reports it). -1 if op is NULL.                               */
 int tpl_op_flags(tpl_op_t op);
 /* Locality order (single-GPU operators; rebuilds the layout). mode 1: the device
  * holds P A P^T, the short rows sorted by the long rows (hub columns) they reference
@@ -111,6 +135,14 @@ tpl_status tpl_op_permutation(tpl_op_t op, int32_t* perm);
  * oracle given its own permutation); untuned operators are deterministic.          */
 tpl_status tpl_op_tune_order(tpl_op_t op, const int32_t* groups, int32_t count, int32_t iters,
                              int32_t* chosen, double* best_us);
+/* Pin the locality order's group count (single GPU; rebuilds the layout; 0 = the
+ * default 16). Deterministic: operators of one matrix with one group count hold the
+ * same order on every device and process, so their results are bit-identical. The
+ * bench pins the count per instance (bench.py PINNED_ORDER_GROUPS, chosen offline from
+ * profiles/r02_group_sweep.txt) instead of tuning on the box.                       */
+tpl_status tpl_op_set_order_groups(tpl_op_t op, int32_t groups);
+/* The group count of the order the device holds (0: caller's order; -1: NULL op). */
+int32_t tpl_op_order_groups(tpl_op_t op);
 /* The locality order's rule alone (host only, no device): perm (n entries) as
  * tpl_op_permutation would report it for this CSR (columns ascending per row),
  * short-row threshold (<= 0: auto) and group count (<= 0: 16); *applied = 0 when the

@@ -18,12 +18,12 @@ tail -2 "$OUT/bench.log"
 [ "${SKIP_PROF:-0}" = "1" ] && exit $rc
 echo "== rocprofv3 kernel trace"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 3 --warmup 1 --cpu-baseline 0 --other-configs 0 > "$OUT/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 4; }
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 5 --warmup 1 --headline-only 1 > "$OUT/prof.log" 2>&1 || { echo "rocprof failed"; tail -20 "$OUT/prof.log"; exit 4; }
 find "$OUT/prof" -name '*stats*' | head
 [ "${SKIP_PMC:-0}" = "1" ] && exit $rc
 echo "== rocprofv3 PMC (FETCH_SIZE, WRITE_SIZE: separate passes)"
 for c in FETCH_SIZE WRITE_SIZE; do
-  timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/pmc_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --cpu-baseline 0 --profile-iters 10 --other-configs 0 --one-pass 0 > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; tail -5 "$OUT/pmc_$c.log"; exit 5; }
+  timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/pmc_$c" -o run --output-format csv -- python3 "$ROOT/bench.py" --steps 1 --warmup 0 --headline-only 1 > "$OUT/pmc_$c.log" 2>&1 || { echo "pmc $c failed"; tail -5 "$OUT/pmc_$c.log"; exit 5; }
 done
 python3 "$ROOT/scripts/pmc_summary.py" $(find "$OUT" -path '*pmc_*' -name '*counter_collection*') > "$OUT/pmc_summary.txt"
 cat "$OUT/pmc_summary.txt"

@@ -35,6 +35,26 @@ static double entry(const tpl_csr_host& A, int64_t i, int64_t j) {
   return 0.0;
 }
 
+// tpl_last_error_detail: status, message and the variant's fields (src/error.rs:20-58)
+static tpl_error_detail detail() {
+  tpl_error_detail d{};
+  if (tpl_last_error_detail(&d) != TPL_OK) std::printf("FAIL: tpl_last_error_detail\n"), ++g_fail;
+  return d;
+}
+
+// host f(T_k) returning one entry too few (-> ParameterMismatch y_k_prime), or an error
+static int short_f(const double*, size_t na, const double*, size_t, double* y, size_t, size_t* len,
+                   char*, size_t, void*) {
+  for (size_t i = 0; i + 1 < na; ++i) y[i] = 0.0;
+  *len = na - 1;
+  return 0;
+}
+static int failing_f(const double*, size_t, const double*, size_t, double*, size_t, size_t*,
+                     char* err, size_t ecap, void*) {
+  std::snprintf(err, ecap, "custom solver failed");
+  return 1;
+}
+
 // host f(T_k) callback that forwards to the built-in inv (so the solve takes the host path)
 static int host_inv(const double* a, size_t na, const double* b, size_t nb, double* y, size_t cap,
                     size_t* len, char* err, size_t ecap, void* user) {
@@ -64,6 +84,28 @@ static void cpu_checks(const char* dmx, const char* qfc, tpl_csr_host& A) {
   CHECK(st == TPL_ERR_DATA_LOADER, "missing file status %d", (int)st);
   CHECK(std::string(tpl_last_error()) == "I/O error: No such file or directory (os error 2)",
         "message '%s'", tpl_last_error());
+  tpl_error_detail d = detail();
+  CHECK(d.status == TPL_ERR_DATA_LOADER && std::string(d.message) == tpl_last_error() &&
+            std::string(d.param_name).empty(), "loader detail %d", (int)d.status);
+  CHECK(tpl_last_error_detail(nullptr) == TPL_ERR_INVALID_ARGUMENT, "detail(NULL)");
+  // malformed CSR on the host-only locality order (decreasing row_ptr, column out of
+  // range, NULL columns): rejected before any indexing
+  {
+    const int64_t rp_bad[3] = {0, 2, 1};
+    const int64_t rp_ok[3] = {0, 1, 2};
+    const int32_t col_ok[2] = {1, 0}, col_oob[2] = {1, 7};
+    int32_t perm[2], applied = -1;
+    CHECK(tpl_locality_order(2, rp_bad, col_ok, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+          "locality_order: decreasing row_ptr");
+    CHECK(tpl_locality_order(2, rp_ok, col_oob, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+          "locality_order: column out of range");
+    CHECK(tpl_locality_order(2, rp_ok, nullptr, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+          "locality_order: NULL columns");
+    CHECK(detail().status == TPL_ERR_INVALID_ARGUMENT, "invalid-argument detail");
+    CHECK(tpl_locality_order(2, rp_ok, col_ok, 0, 0, perm, &applied) == TPL_OK, "locality_order ok");
+    d = detail();
+    CHECK(d.status == TPL_OK && std::string(d.message).empty(), "detail after success");
+  }
   // built-in f(T_k) (include/tpl.h): T = [[2,1],[1,2]]
   const double al[2] = {2.0, 2.0}, be[1] = {1.0};
   double y[2];
@@ -125,11 +167,43 @@ static void gpu_checks(tpl_csr_host& A) {
   uint64_t bytes = 0;
   CHECK(tpl_op_device_bytes(op, &bytes) == TPL_OK && bytes >= (uint64_t)(8 * n * 50), "device bytes %llu",
         (unsigned long long)bytes);
+  // every LanczosErrorKind the engine raises, with its fields (tpl_last_error_detail)
   std::vector<double> z(n, 0.0);
   CHECK(tpl_lanczos_two_pass(op, z.data(), n, 5, tpl_ftk_inv, nullptr, x1.data(), TPL_MEM_HOST) ==
             TPL_ERR_INPUT, "zero b");
+  tpl_error_detail d = detail();
+  CHECK(d.status == TPL_ERR_INPUT &&
+            std::string(d.inner) == "Input vector `b` must not be a zero vector." &&
+            std::string(d.message) == "Invalid input parameter: " + std::string(d.inner),
+        "InputError detail '%s'", d.inner);
   CHECK(tpl_lanczos_two_pass(op, b.data(), n - 1, 5, tpl_ftk_inv, nullptr, x1.data(), TPL_MEM_HOST) ==
             TPL_ERR_DIMENSION_MISMATCH, "dimension");
+  d = detail();
+  CHECK(d.status == TPL_ERR_DIMENSION_MISMATCH && d.operator_cols == (uint64_t)n &&
+            d.vector_rows == (uint64_t)(n - 1), "DimensionMismatch detail %llu %llu",
+        (unsigned long long)d.operator_cols, (unsigned long long)d.vector_rows);
+  CHECK(tpl_lanczos_two_pass(op, b.data(), n, 20, short_f, nullptr, x1.data(), TPL_MEM_HOST) ==
+            TPL_ERR_PARAMETER_MISMATCH, "y_k_prime mismatch");
+  d = detail();
+  CHECK(d.status == TPL_ERR_PARAMETER_MISMATCH && std::string(d.param_name) == "y_k_prime" &&
+            d.expected == 20 && d.actual == 19 &&
+            std::string(d.message) == "Parameter mismatch: `y_k_prime` expects size 20, but got 19.",
+        "ParameterMismatch(y_k_prime) detail '%s' %llu %llu", d.param_name,
+        (unsigned long long)d.expected, (unsigned long long)d.actual);
+  CHECK(tpl_lanczos_two_pass(op, b.data(), n, 20, failing_f, nullptr, x1.data(), TPL_MEM_HOST) ==
+            TPL_ERR_SOLVER, "solver error");
+  d = detail();
+  CHECK(d.status == TPL_ERR_SOLVER && std::string(d.inner) == "custom solver failed" &&
+            std::string(d.message) == "The user-provided f(T_k) solver failed: custom solver failed",
+        "SolverError detail '%s'", d.message);
+  {
+    double al[4] = {0, 0, 0, 0}, be[3] = {1, 1, 1}, yk[3] = {1, 0, 0};
+    CHECK(tpl_lanczos_pass_two(op, b.data(), n, al, 4, be, 3, 4, 1.0, yk, 3, x1.data(), nullptr,
+                               TPL_MEM_HOST) == TPL_ERR_PARAMETER_MISMATCH, "y_k mismatch");
+    d = detail();
+    CHECK(d.status == TPL_ERR_PARAMETER_MISMATCH && std::string(d.param_name) == "y_k" &&
+              d.expected == 4 && d.actual == 3, "ParameterMismatch(y_k) detail");
+  }
   tpl_op_destroy(op);
   tpl_ctx_destroy(ctx);
 }

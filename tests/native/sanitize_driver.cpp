@@ -236,6 +236,59 @@ static void layout_checks() {
   }
 }
 
+// tpl_locality_order (host-only C ABI entry): malformed CSRs are rejected before any
+// indexing (decreasing row_ptr, row_ptr[0] != 0, columns out of range or not ascending,
+// NULL columns), and 300 random mutations of valid CSRs never read out of bounds —
+// either rejected or a permutation.
+static void locality_abi_checks() {
+  int32_t perm[8], applied = -1;
+  const int64_t rp_dec[4] = {0, 3, 1, 4}, rp_start[4] = {1, 2, 3, 4}, rp_ok[4] = {0, 2, 3, 4};
+  const int32_t col_ok[4] = {1, 2, 0, 0}, col_neg[4] = {-1, 2, 0, 0}, col_big[4] = {1, 9, 0, 0},
+                col_desc[4] = {2, 1, 0, 0};
+  CHECK(tpl_locality_order(3, rp_dec, col_ok, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+        "decreasing row_ptr accepted");
+  CHECK(tpl_locality_order(3, rp_start, col_ok, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+        "row_ptr[0] != 0 accepted");
+  CHECK(tpl_locality_order(3, rp_ok, col_neg, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+        "negative column accepted");
+  CHECK(tpl_locality_order(3, rp_ok, col_big, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+        "column >= n accepted");
+  CHECK(tpl_locality_order(3, rp_ok, col_desc, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+        "descending columns accepted");
+  CHECK(tpl_locality_order(3, rp_ok, nullptr, 0, 0, perm, &applied) == TPL_ERR_INVALID_ARGUMENT,
+        "NULL columns accepted");
+  CHECK(tpl_locality_order(3, rp_ok, col_ok, 0, 0, perm, &applied) == TPL_OK, "valid CSR: %s",
+        tpl_last_error());
+  std::mt19937_64 rng(77);
+  int accepted = 0;
+  for (int it = 0; it < 300; ++it) {
+    std::vector<int32_t> rp32, col;
+    std::vector<double> val;
+    const int64_t n = 2 + (int64_t)(rng() % 400);
+    random_csr(n, (int)(rng() % 3), 40 + (int)(rng() % 100), rng(), rp32, col, val);
+    std::vector<int64_t> rp(rp32.begin(), rp32.end());
+    const int kind = (int)(rng() % 4);  // 0: none, 1: row_ptr, 2: column value, 3: swap
+    if (kind == 1) rp[1 + rng() % n] += (int64_t)(rng() % 7) - 3;
+    if (kind == 2 && !col.empty()) col[rng() % col.size()] = (int32_t)(rng() % (3 * n)) - (int32_t)n;
+    if (kind == 3 && col.size() > 1) {
+      const size_t q = rng() % (col.size() - 1);
+      std::swap(col[q], col[q + 1]);
+    }
+    if (rp[n] > (int64_t)col.size()) continue;  // row_ptr[n] is the caller's nnz: keep it readable
+    std::vector<int32_t> pm(n, -1);
+    const tpl_status st = tpl_locality_order(n, rp.data(), col.empty() ? nullptr : col.data(), 0,
+                                             (int)(rng() % 20), pm.data(), &applied);
+    CHECK(st == TPL_OK || st == TPL_ERR_INVALID_ARGUMENT, "mutation %d: status %d", it, (int)st);
+    if (st != TPL_OK) continue;
+    ++accepted;
+    std::vector<char> seen(n, 0);
+    bool ok = true;
+    for (int64_t i = 0; ok && i < n; ++i) ok = pm[i] >= 0 && pm[i] < n && !seen[pm[i]]++;
+    CHECK(ok, "mutation %d: not a permutation", it);
+  }
+  CHECK(accepted > 50, "only %d valid mutations", accepted);
+}
+
 int main(int argc, char** argv) {
   if (argc < 4) {
     std::printf("usage: sanitize_driver <dmx> <qfc> <scratch dir>\n");
@@ -244,6 +297,7 @@ int main(int argc, char** argv) {
   loader_checks(argv[1], argv[2], argv[3]);
   ftk_checks();
   layout_checks();
+  locality_abi_checks();
   std::printf("%s (%d failures)\n", g_fail ? "FAILED" : "OK", g_fail);
   return g_fail ? 1 : 0;
 }

@@ -64,6 +64,49 @@ def test_version_and_no_device_is_reported_cleanly():
             tpl_amd.HipCsrOp(sp.identity(3).tocsr())
 
 
+def test_error_detail_rebuilds_every_variant():
+    """tpl_last_error_detail (the fields of a LanczosErrorKind across the C ABI): the
+    Python mirror rebuilds each variant from the fields alone and gets the reference's
+    Display text; a host-only call records its status, and success resets it."""
+    from tpl_amd.error import from_detail
+    base = {"status": 0, "message": "", "inner": "", "param_name": "", "expected": 0,
+            "actual": 0, "operator_cols": 0, "vector_rows": 0, "breakdown_step": 0}
+    cases = [
+        (dict(status=_lib.TPL_ERR_PARAMETER_MISMATCH, param_name="y_k", expected=10, actual=9),
+         "Parameter mismatch: `y_k` expects size 10, but got 9."),
+        (dict(status=_lib.TPL_ERR_DIMENSION_MISMATCH, operator_cols=100, vector_rows=99),
+         "Dimension mismatch: operator has 100 columns but vector has 99 rows."),
+        (dict(status=_lib.TPL_ERR_INPUT, inner="The initial vector `b` must not be a zero vector."),
+         "Invalid input parameter: The initial vector `b` must not be a zero vector."),
+        (dict(status=_lib.TPL_ERR_SOLVER, inner="Custom solver failed"),
+         "The user-provided f(T_k) solver failed: Custom solver failed"),
+        (dict(status=_lib.TPL_ERR_EVD, inner="NoConvergence"),
+         "A numerical error occurred during the eigendecomposition of T_k: NoConvergence"),
+        (dict(status=_lib.TPL_ERR_BREAKDOWN, breakdown_step=42),
+         "Lanczos iteration breakdown at step 42: Beta coefficient is zero. The Krylov "
+         "subspace is invariant."),
+    ]
+    for fields, text in cases:
+        assert str(from_detail({**base, **fields})) == text
+    # a real failure through the C ABI (host-only entry point: no GPU needed)
+    from ctypes import POINTER, byref, c_int32, c_int64
+    rp = np.array([0, 2, 1], dtype=np.int64)  # decreasing row_ptr
+    ci = np.array([1, 0], dtype=np.int32)
+    perm = np.zeros(2, dtype=np.int32)
+    applied = c_int32()
+    st = _lib.tpl_locality_order(2, rp.ctypes.data_as(POINTER(c_int64)),
+                                 ci.ctypes.data_as(POINTER(c_int32)), 0, 0,
+                                 perm.ctypes.data_as(POINTER(c_int32)), byref(applied))
+    assert st == _lib.TPL_ERR_INVALID_ARGUMENT
+    d = _lib.last_error_detail()
+    assert d["status"] == st and d["message"] == _lib.last_error() == "row_ptr not monotone"
+    rp[:] = [0, 1, 2]
+    assert _lib.tpl_locality_order(2, rp.ctypes.data_as(POINTER(c_int64)),
+                                   ci.ctypes.data_as(POINTER(c_int32)), 0, 0,
+                                   perm.ctypes.data_as(POINTER(c_int32)), byref(applied)) == 0
+    assert _lib.last_error_detail()["status"] == 0
+
+
 @pytest.mark.parametrize("arcs", [5000, 50000, 500000])
 def test_fixture_md5(arcs):
     assert md5_of_xz(os.path.join(KKT_DIR, f"netgen-{arcs}-3.dmx.xz")) == KKT_MD5[arcs]

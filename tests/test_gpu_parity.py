@@ -9,6 +9,9 @@ Parity contract:
       for configs 1-2 (before the order-chaos onset), the reference's own thresholds
       (5e-9 property checks, 1e-3 / 1e-12 analytic checks) everywhere
 """
+import os
+import sys
+
 import numpy as np
 import pytest
 import scipy.sparse as sp
@@ -30,6 +33,9 @@ from tpl_amd import algorithms as alg  # noqa: E402
 def _need_gpu():
     if tpl_amd.device_count() < 1:
         pytest.skip("no GPU visible")
+
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def canon(op: HipCsrOp, a):
@@ -292,6 +298,8 @@ def test_error_semantics(op5k, kkt5k):
     with pytest.raises(LanczosError) as e:
         alg.lanczos_pass_two(op5k, b, d, np.ones(5))
     assert str(e.value) == "Parameter mismatch: `y_k` expects size 6, but got 5."
+    # the variant's fields crossed the C ABI (tpl_last_error_detail), not just its text
+    assert e.value.payload == {"param_name": "y_k", "expected": 6, "actual": 5}
     d0 = alg.LanczosDecomposition(d.alphas, d.betas, d.steps_taken, 0.0)
     with pytest.raises(LanczosError) as e:
         alg.lanczos_pass_two(op5k, b, d0, np.ones(6))
@@ -303,15 +311,19 @@ def test_error_semantics(op5k, kkt5k):
     with pytest.raises(LanczosError) as e:
         solvers.lanczos_two_pass(op5k, b, 5, bad)
     assert str(e.value) == "The user-provided f(T_k) solver failed: boom"
+    assert e.value.kind == LanczosErrorKind.SOLVER_ERROR and e.value.payload == "boom"
     with pytest.raises(LanczosError) as e:
         solvers.lanczos(op5k, b, 5, lambda al, be: np.ones(3))
     assert str(e.value) == "Parameter mismatch: `y_k_prime` expects size 5, but got 3."
+    assert e.value.payload == {"param_name": "y_k_prime", "expected": 5, "actual": 3}
     with pytest.raises(LanczosError) as e:
         solvers.lanczos_two_pass(op5k, b, 5, lambda al, be: np.ones((5, 2)))
     assert e.value.kind == LanczosErrorKind.PARAMETER_MISMATCH
     with pytest.raises(LanczosError) as e:
         solvers.lanczos_two_pass(op5k, b[:-1], 5, ftk.INV)
     assert str(e.value) == f"Dimension mismatch: operator has {n} columns but vector has {n - 1} rows."
+    assert e.value.kind == LanczosErrorKind.DIMENSION_MISMATCH
+    assert e.value.payload == {"operator_cols": n, "vector_rows": n - 1}
     with pytest.raises(LanczosError) as e:
         solvers.lanczos_two_pass(op5k, b, 0, ftk.INV)
     assert e.value.kind == LanczosErrorKind.INPUT_ERROR
@@ -488,6 +500,39 @@ def test_headline_500k_bitwise(kkt_tmp):
     xo, _ = o.pass_two(b, al, be, s, bn, ftk.INV(al, be) * bn)
     assert np.array_equal(x, xo)
     assert np.linalg.norm(a @ x - b) / np.linalg.norm(b) < 1e-8
+
+
+def test_headline_pinned_order_bitwise(kkt_tmp):
+    """The operator the bench times, exactly: 500k arcs in the locality order with the
+    pinned group count (bench.py PINNED_ORDER_GROUPS), two-pass k = 500, f = inv (the
+    one-graph host-f path the bench takes at k = 500). alpha / beta / x are bitwise the
+    canonical oracle's on that permutation, and a second operator built the same way
+    (what the next bench run builds) reproduces x bit for bit."""
+    sys.path.insert(0, ROOT)
+    from bench import PINNED_ORDER_GROUPS
+    g = PINNED_ORDER_GROUPS[500000]
+    kkt = load_kkt(500000, kkt_tmp)
+    a = kkt.a
+    b = harness_b(a)
+    op = HipCsrOp(a)
+    op.set_order_groups(g)
+    assert op.flags() & 64 and op.order_groups() == g
+    sch = op.schedule()
+    import tpl_amd
+    assert np.array_equal(sch["perm"], tpl_amd.locality_order(a, groups=g))
+    o = oracle.Operator(a, sch)
+    d = alg.lanczos_pass_one(op, b, 500)
+    al, be, s, bn, _ = o.pass_one(b, 500)
+    assert d.steps_taken == s == 500 and d.b_norm == bn
+    assert np.array_equal(d.alphas, al) and np.array_equal(d.betas, be)
+    x = solvers.lanczos_two_pass(op, b, 500, ftk.INV)
+    xo, _ = o.pass_two(b, al, be, s, bn, ftk.INV(al, be) * bn)
+    assert np.array_equal(x, xo)
+    op2 = HipCsrOp(a)
+    op2.set_order_groups(g)
+    assert np.array_equal(solvers.lanczos_two_pass(op2, b, 500, ftk.INV), x)
+    op.close()
+    op2.close()
 
 
 def test_int8_value_format_bitwise(kkt_tmp):

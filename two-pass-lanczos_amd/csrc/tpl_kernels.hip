@@ -586,9 +586,13 @@ __global__ __launch_bounds__(kTPB) void k_reorth_update(int64_t n, int cols,
 // of r's squared norm. n0 = ||r||^2 (the partials k_p1_axpy left in S.Pb), n1 = ||r'||^2
 // (Pb1, written by the first update), both reduced in the canonical norm order; if
 // n1 >= n0 / 2 the second pass is skipped and r' is the result — its partials become the
-// ones k_p1_spmv reduces for beta — else S.flags[3] counts a second pass. One workgroup.
+// ones k_p1_spmv reduces for beta — else S.flags[3] counts a second pass. rec: this
+// step's slot of the per-step record (1: a second pass ran), so the host can count only
+// the steps a caller keeps (a step callback may stop before the device's last step).
+// One workgroup.
 __global__ __launch_bounds__(kTPB) void k_reorth_decide(DevState S, const double* __restrict__ Pb1,
-                                                        int G2, int* __restrict__ skip) {
+                                                        int G2, int* __restrict__ skip,
+                                                        int* __restrict__ rec) {
   __shared__ double red[4];
   PartialRegs<4> p0, p1;  // G2 <= 1024
   load_partials(S.Pb, G2, p0);
@@ -600,6 +604,7 @@ __global__ __launch_bounds__(kTPB) void k_reorth_decide(DevState S, const double
     for (int i = threadIdx.x; i < G2; i += kTPB) S.Pb[i] = Pb1[i];
   if (threadIdx.x == 0) {
     *skip = sk ? 1 : 0;
+    *rec = sk ? 0 : 1;
     if (!sk) S.flags[3] = S.flags[3] + 1;
   }
 }
@@ -754,8 +759,9 @@ hipError_t reorth_update(int64_t n, int cols, const double* V, double* r, const 
                      skip);
   return hipGetLastError();
 }
-hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip, hipStream_t s) {
-  hipLaunchKernelGGL(k_reorth_decide, dim3(1), dim3(kTPB), 0, s, S, Pb1, G2, skip);
+hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip, int* rec,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k_reorth_decide, dim3(1), dim3(kTPB), 0, s, S, Pb1, G2, skip, rec);
   return hipGetLastError();
 }
 

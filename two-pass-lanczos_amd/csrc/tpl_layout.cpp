@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <new>
 #include <string>
 #include <utility>
 #include <vector>
@@ -55,40 +56,11 @@ std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
     if (is_long) rank[i] = n_long++;
   }
   if (n_long == 0) return {};
-  const int32_t G = std::max(1, sp.order_groups);
-  const int32_t gsize = (n_long + G - 1) / G;  // long-row ranks per group
-  struct Key {
-    int32_t tail, glo, ghi, rlo, rhi, row;
-  };
-  std::vector<Key> keys;
-  keys.reserve(n - n_long);
-  for (int64_t i = 0; i < n; ++i) {
-    if (rank[i] >= 0) continue;
-    int32_t lo = INT32_MAX, hi = INT32_MAX;  // no long reference: after the others
-    int32_t tail = 0;
-    for (int32_t q = rp[i]; q < rp[i + 1]; ++q) {
-      const int32_t r = rank[col[q]];
-      if (r < 0) {
-        tail |= col[q] != i;  // references another short row
-        continue;
-      }
-      if (lo == INT32_MAX) lo = r;
-      hi = r;  // columns ascend and ranks follow the row order
-    }
-    auto grp = [&](int32_t r) { return r == INT32_MAX ? INT32_MAX : r / gsize; };
-    keys.push_back(Key{tail, grp(lo), grp(hi), lo, hi, (int32_t)i});
-  }
-  std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
-    if (x.tail != y.tail) return x.tail < y.tail;
-    if (x.glo != y.glo) return x.glo < y.glo;
-    if (x.ghi != y.ghi) return x.ghi < y.ghi;
-    if (x.rlo != y.rlo) return x.rlo < y.rlo;
-    if (x.rhi != y.rhi) return x.rhi < y.rhi;
-    return x.row < y.row;
-  });
   std::vector<int32_t> perm;
   perm.reserve(n);
-  for (const Key& k : keys) perm.push_back(k.row);
+  for (int64_t i = 0; i < n; ++i)
+    if (rank[i] < 0) perm.push_back((int32_t)i);
+  locality_sort(perm, rp.data(), col.data(), rank.data(), n_long, sp.order_groups);
   for (int64_t i = 0; i < n; ++i)
     if (rank[i] >= 0) perm.push_back((int32_t)i);
   bool identity = true;
@@ -321,4 +293,55 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   return L;
 }
 
+// The CSR rules of every entry point that takes a matrix: row_ptr (n + 1 entries) starts
+// at 0 and is monotone; col_idx is non-NULL when there are entries; every column lies in
+// [0, n_cols) and the columns of a row ascend strictly.
+void check_csr(int64_t n, int64_t n_cols, const int64_t* row_ptr, const int32_t* col_idx) {
+  if (row_ptr[0] != 0) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0 and end at nnz");
+  for (int64_t i = 0; i < n; ++i)
+    if (row_ptr[i + 1] < row_ptr[i]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
+  if (row_ptr[n] > 0 && !col_idx) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+      const int32_t c = col_idx[q];
+      if (c < 0 || c >= n_cols) fail(TPL_ERR_INVALID_ARGUMENT, "column index out of range");
+      if (q > row_ptr[i] && c <= col_idx[q - 1])
+        fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be strictly ascending per row");
+    }
+}
+
 } // namespace tpl
+
+// Host-only C ABI entry (include/tpl.h): the locality order's permutation of a CSR.
+extern "C" tpl_status tpl_locality_order(int64_t n, const int64_t* row_ptr,
+                                         const int32_t* col_idx, int32_t short_row_max,
+                                         int32_t groups, int32_t* perm, int32_t* applied) {
+  using namespace tpl;
+  try {
+    if (n < 0 || (n > 0 && (!row_ptr || !perm)) || !applied)
+      fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
+    if (n >= INT32_MAX || (n > 0 && row_ptr[n] >= INT32_MAX))
+      fail(TPL_ERR_UNSUPPORTED, "n and nnz must be < 2^31");
+    // the operator constructors' CSR rules: row_ptr from 0, monotone; columns in range,
+    // strictly ascending per row (short_row_threshold and the sort key index by them)
+    if (n > 0) check_csr(n, n, row_ptr, col_idx);
+    std::vector<int32_t> rp(n + 1, 0);
+    for (int64_t i = 0; n > 0 && i <= n; ++i) rp[i] = (int32_t)row_ptr[i];
+    std::vector<int32_t> col;
+    if (n > 0 && row_ptr[n] > 0) col.assign(col_idx, col_idx + row_ptr[n]);
+    SchedParams sp;
+    sp.short_row_max = short_row_max > 0 ? short_row_max : -1;
+    if (groups > 0) sp.order_groups = groups;
+    const std::vector<int32_t> p = locality_order(n, rp, col, sp);
+    *applied = p.empty() ? 0 : 1;
+    for (int64_t i = 0; i < n; ++i) perm[i] = p.empty() ? (int32_t)i : p[i];
+    set_last_error("");
+    return TPL_OK;
+  } catch (const Error& e) {
+    set_last_error(e.code, e.msg, e.det);
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    set_last_error(TPL_ERR_OUT_OF_MEMORY, "host allocation failed", {});
+    return TPL_ERR_OUT_OF_MEMORY;
+  }
+}

@@ -80,12 +80,57 @@ int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int reque
 // of a node's arcs hit lines their neighbours have just fetched.
 std::vector<int32_t> locality_order(int64_t n, const std::vector<int32_t>& rp,
                                     const std::vector<int32_t>& col, const SchedParams& sp);
+
+// The locality order's sort of short rows (shared by locality_order and the replicated
+// partition's per-rank order, tpl_dist_op_create_replicated): `rows` (indices into the
+// CSR rp / col, columns ascending per row) are sorted by the key above, given lrank[c] =
+// the rank of column c among the n_long long rows (-1: a short row) and G groups.
+template <class RowPtr, class Row>
+void locality_sort(std::vector<Row>& rows, const RowPtr* rp, const int32_t* col,
+                   const int32_t* lrank, int32_t n_long, int32_t G) {
+  const int32_t gsize = (n_long + std::max(1, G) - 1) / std::max(1, G);  // ranks per group
+  struct Key {
+    int32_t tail, glo, ghi, rlo, rhi;
+    Row row;
+  };
+  std::vector<Key> keys;
+  keys.reserve(rows.size());
+  for (const Row i : rows) {
+    int32_t lo = INT32_MAX, hi = INT32_MAX;  // no long reference: after the others
+    int32_t tail = 0;
+    for (RowPtr q = rp[i]; q < rp[i + 1]; ++q) {
+      const int32_t r = lrank[col[q]];
+      if (r < 0) {
+        tail |= (Row)col[q] != i;  // references another short row
+        continue;
+      }
+      if (lo == INT32_MAX) lo = r;
+      hi = r;  // columns ascend and ranks follow the row order
+    }
+    auto grp = [&](int32_t r) { return r == INT32_MAX ? INT32_MAX : r / gsize; };
+    keys.push_back(Key{tail, grp(lo), grp(hi), lo, hi, i});
+  }
+  std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
+    if (x.tail != y.tail) return x.tail < y.tail;
+    if (x.glo != y.glo) return x.glo < y.glo;
+    if (x.ghi != y.ghi) return x.ghi < y.ghi;
+    if (x.rlo != y.rlo) return x.rlo < y.rlo;
+    if (x.rhi != y.rhi) return x.rhi < y.rhi;
+    return x.row < y.row;
+  });
+  for (size_t p = 0; p < keys.size(); ++p) rows[p] = keys[p].row;
+}
 // P A P^T in CSR: internal row i = the caller's row perm[i], columns mapped through
 // iperm (the inverse) and re-sorted ascending.
 void permute_csr(int64_t n, const std::vector<int32_t>& rp, const std::vector<int32_t>& col,
                  const std::vector<double>& val, const std::vector<int32_t>& perm,
                  const std::vector<int32_t>& iperm, std::vector<int32_t>& prp,
                  std::vector<int32_t>& pcol, std::vector<double>& pval);
+
+// Throws tpl::Error (TPL_ERR_INVALID_ARGUMENT) unless row_ptr (n + 1 entries) starts at
+// 0 and is monotone, col_idx is non-NULL when row_ptr[n] > 0, and every row's columns lie
+// in [0, n_cols) strictly ascending.
+void check_csr(int64_t n, int64_t n_cols, const int64_t* row_ptr, const int32_t* col_idx);
 
 // n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds are
 // taken on global column indices, so a partition of one rank reproduces the single-GPU

@@ -286,10 +286,10 @@ tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_c
     tpl::set_last_error("");
     return TPL_OK;
   } catch (const tpl::Error& e) {
-    tpl::set_last_error(e.msg);
+    tpl::set_last_error(e.code, e.msg, e.det);
     return e.code;
   } catch (const std::bad_alloc&) {
-    tpl::set_last_error("host allocation failed");
+    tpl::set_last_error(TPL_ERR_OUT_OF_MEMORY, "host allocation failed", {});
     return TPL_ERR_OUT_OF_MEMORY;
   }
 }
@@ -327,10 +327,10 @@ tpl_status tpl_generate_kkt(int64_t num_arcs, int64_t num_nodes, uint64_t seed,
     tpl::set_last_error("");
     return TPL_OK;
   } catch (const tpl::Error& e) {
-    tpl::set_last_error(e.msg);
+    tpl::set_last_error(e.code, e.msg, e.det);
     return e.code;
   } catch (const std::bad_alloc&) {
-    tpl::set_last_error("host allocation failed");
+    tpl::set_last_error(TPL_ERR_OUT_OF_MEMORY, "host allocation failed", {});
     return TPL_ERR_OUT_OF_MEMORY;
   }
 }

@@ -53,7 +53,8 @@ hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, i
                        const double* v_cur, const double* v_prev, double* v_next, double* x,
                        double* Vcol, int j, int nflush, hipStream_t s);
 hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hipStream_t s);
-hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip, hipStream_t s);
+hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip, int* rec,
+                         hipStream_t s);
 hipError_t reorth_dot(int64_t n, int cols, const double* V, const double* r, double* P, int G,
                       int64_t E, const int* skip, hipStream_t s);
 hipError_t reorth_reduce(int cols, const double* P, int G, double* h, const int* skip, hipStream_t s);
@@ -76,13 +77,13 @@ static tpl_status guarded(F&& f) {
     set_last_error("");
     return TPL_OK;
   } catch (const Error& e) {
-    set_last_error(e.msg);
+    set_last_error(e.code, e.msg, e.det);
     return e.code;
   } catch (const std::bad_alloc&) {
-    set_last_error("host allocation failed");
+    set_last_error(TPL_ERR_OUT_OF_MEMORY, "host allocation failed", {});
     return TPL_ERR_OUT_OF_MEMORY;
   } catch (const std::exception& e) {
-    set_last_error(e.what());
+    set_last_error(TPL_ERR_INVALID_ARGUMENT, e.what(), {});
     return TPL_ERR_INVALID_ARGUMENT;
   }
 }
@@ -385,8 +386,9 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
   }
   if (reorth && !op->d_Pr) {
     // [cols x G partials][cols coefficients][G norm partials after the first pass][skip flag]
+    // [kcap per-step second-pass records (int)]
     dev_alloc(op, &op->d_Pr,
-              (((size_t)op->lay.G2 + 1) * op->kcap + (size_t)op->lay.G2 + 1) * sizeof(double));
+              (((size_t)op->lay.G2 + 2) * op->kcap + (size_t)op->lay.G2 + 1) * sizeof(double));
   }
 }
 
@@ -405,7 +407,7 @@ void set_device(const tpl_op_s* op) { HIPCHK(hipSetDevice(op->device)); }
 
 void check_b(const tpl_op_s* op, const double* b, int64_t b_len) {
   if (!b && op->n > 0) fail(TPL_ERR_INVALID_ARGUMENT, "b is NULL");
-  if (b_len != op->n) fail(TPL_ERR_DIMENSION_MISMATCH, msg_dimension(op->n, b_len));
+  if (b_len != op->n) fail_dimension(op->n, b_len);
 }
 
 // A caller-order vector into a device vector (internal order).
@@ -489,6 +491,11 @@ void dist_total(tpl_op_s* op, const double* P, int N, double* slot) {
   HIPCHK(launch::reorth_reduce(1, P, N, slot, nullptr, op->stream));
 }
 
+// Per-step second-pass records of the selective re-orthogonalisation (slot j - 1: step j).
+int* reorth_records(const tpl_op_s* op) {
+  return reinterpret_cast<int*>(op->d_Pr + ((size_t)op->lay.G2 + 1) * op->kcap + op->lay.G2 + 1);
+}
+
 // ---- reorthogonalisation (extension, not in the reference): classical Gram-Schmidt of
 // r_{j+1} against the stored columns V[:, 0..j) before beta_j. mode 1 (CGS2): two
 // passes, always. mode 2 (selective, Kahan–Parlett "twice is enough"): the second pass
@@ -503,6 +510,7 @@ void enqueue_reorth(tpl_op_s* op, int j, int mode) {
   double* h = op->d_Pr + (size_t)G2 * op->kcap;    // cols coefficients
   double* Pb1 = h + op->kcap;                      // ||r'||^2 partials (selective)
   int* skip = reinterpret_cast<int*>(Pb1 + G2);
+  int* rec = reorth_records(op) + (j - 1);
   double* r = op->R[(j + 1) % 3];
   for (int pass = 0; pass < 2; ++pass) {
     const int* sk = (mode == 2 && pass == 1) ? skip : nullptr;
@@ -512,7 +520,8 @@ void enqueue_reorth(tpl_op_s* op, int j, int mode) {
     // selective mode the first one writes its own partials for the decision
     double* pn = pass == 1 ? op->S.Pb : (mode == 2 ? Pb1 : nullptr);
     HIPCHK(launch::reorth_update(op->n, cols, op->d_V, r, h, pn, G2, E, sk, op->stream));
-    if (mode == 2 && pass == 0) HIPCHK(launch::reorth_decide(op->S, Pb1, G2, skip, op->stream));
+    if (mode == 2 && pass == 0)
+      HIPCHK(launch::reorth_decide(op->S, Pb1, G2, skip, rec, op->stream));
   }
 }
 
@@ -764,7 +773,7 @@ void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV,
 void check_k(size_t k) {
   // The reference panics at k = 0 (Vec::with_capacity(k - 1) underflow,
   // src/algorithms/lanczos.rs:75); the C ABI reports it instead.
-  if (k == 0) fail(TPL_ERR_INPUT, msg_input("The number of iterations `k` must be at least 1."));
+  if (k == 0) fail_input("The number of iterations `k` must be at least 1.");
   if (k > (size_t)INT32_MAX / 2) fail(TPL_ERR_INVALID_ARGUMENT, "k too large");
 }
 
@@ -777,9 +786,9 @@ void call_ftk(tpl_ftk_fn f, void* user, const HostDecomp& d, std::vector<double>
   const int rc = f(d.alphas, d.steps, d.betas, d.steps > 0 ? d.steps - 1 : 0, y.data(), d.steps,
                    &ylen, err, sizeof(err), user);
   err[sizeof(err) - 1] = '\0';
-  if (rc != 0) fail(TPL_ERR_SOLVER, msg_solver(err));
+  if (rc != 0) fail_solver(err);
   if (ylen != d.steps)
-    fail(TPL_ERR_PARAMETER_MISMATCH, msg_param_mismatch("y_k_prime", d.steps, ylen));
+    fail_param_mismatch("y_k_prime", d.steps, ylen);
 }
 
 void zero_out(tpl_op_s* op, double* x_out, int mem) {
@@ -910,18 +919,9 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
     if (n >= INT32_MAX || nnz >= INT32_MAX)
       fail(TPL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 (int32 device offsets)");
     if (!row_ptr) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr is NULL");
-    if (nnz > 0 && (!col_idx || !vals)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
-    if (row_ptr[0] != 0 || row_ptr[n] != nnz)
-      fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0 and end at nnz");
-    for (int64_t i = 0; i < n; ++i) {
-      if (row_ptr[i + 1] < row_ptr[i]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
-      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
-        const int32_t c = col_idx[q];
-        if (c < 0 || c >= n) fail(TPL_ERR_INVALID_ARGUMENT, "column index out of range");
-        if (q > row_ptr[i] && c <= col_idx[q - 1])
-          fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be strictly ascending per row");
-      }
-    }
+    if (nnz > 0 && !vals) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    if (row_ptr[n] != nnz) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0 and end at nnz");
+    check_csr(n, n, row_ptr, col_idx);
     HIPCHK(hipSetDevice(ctx->device));
     auto op = std::make_unique<tpl_op_s>();
     op->ctx = ctx;
@@ -1025,7 +1025,7 @@ tpl_status tpl_lanczos_pass_one(tpl_op_t op, const double* b, int64_t b_len, siz
     check_k(k);
     run_pass_one(op, b, k, mem, false, false);
     const HostDecomp d = fetch_decomp(op, k);
-    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    if (d.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
     std::memcpy(alphas, d.alphas, d.steps * sizeof(double));
     if (d.steps > 1) std::memcpy(betas, d.betas, (d.steps - 1) * sizeof(double));
     *steps = d.steps;
@@ -1104,13 +1104,20 @@ tpl_status tpl_lanczos_standard(tpl_op_t op, const double* b, int64_t b_len, siz
       d = fetch_decomp(op, k);
       d.steps = std::min(d.steps, stop_at);
     }
-    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    if (d.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
     std::memcpy(alphas, d.alphas, d.steps * sizeof(double));
     if (d.steps > 1) std::memcpy(betas, d.betas, (d.steps - 1) * sizeof(double));
     *steps = d.steps;
     *b_norm = d.b_norm;
-    op->reorth_second =
-        reorth == 2 ? d.flags[3] : (reorth == 1 && d.steps > 1 ? (int64_t)d.steps - 1 : 0);
+    // second passes of the steps the caller keeps: a step callback may stop before the
+    // device's last step (batched polling runs ahead), so count the kept steps' records
+    op->reorth_second = reorth == 1 && d.steps > 1 ? (int64_t)d.steps - 1 : 0;
+    if (reorth == 2 && d.steps > 1) {
+      std::vector<int> rec(d.steps - 1);
+      HIPCHK(hipMemcpy(rec.data(), reorth_records(op), rec.size() * sizeof(int),
+                       hipMemcpyDeviceToHost));
+      for (int r : rec) op->reorth_second += r;
+    }
     if (v_out && d.steps > 0) {
       download_vec(op, v_out, op->d_V, (int64_t)d.steps, mem);
       sync_checked(op);
@@ -1127,10 +1134,10 @@ tpl_status tpl_lanczos_pass_two(tpl_op_t op, const double* b, int64_t b_len, con
     set_device(op);
     check_b(op, b, b_len);
     // src/algorithms/lanczos_two_pass.rs:220-227
-    if (steps != y_len) fail(TPL_ERR_PARAMETER_MISMATCH, msg_param_mismatch("y_k", steps, y_len));
+    if (steps != y_len) fail_param_mismatch("y_k", steps, y_len);
     // :229-235
     if (b_norm <= kBreakdownTol)
-      fail(TPL_ERR_INPUT, msg_input("The initial vector `b` must not be a zero vector."));
+      fail_input("The initial vector `b` must not be a zero vector.");
     if (steps == 0) { // :237-244
       zero_out(op, x_out, mem);
       return;
@@ -1181,7 +1188,7 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
       sync_checked(op);
       int32_t flags[4];
       std::memcpy(flags, op->h_state, 16);
-      if (flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+      if (flags[1]) fail_input("Input vector `b` must not be a zero vector.");
       if (flags[2] == 0) zero_out(op, x_out, mem);
       return;
     }
@@ -1189,7 +1196,7 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
     op->last_one_graph = false;
     run_pass_one(op, b, k, mem, false, false);
     const HostDecomp d = fetch_decomp(op, k);
-    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    if (d.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
     if (d.steps == 0) { // :150-152
       zero_out(op, x_out, mem);
       return;
@@ -1218,7 +1225,7 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
     // 1. standard pass, V_k in HBM (src/solvers.rs:61)
     run_pass_one(op, b, k, mem, true, false);
     const HostDecomp d = fetch_decomp(op, k);
-    if (d.flags[1]) fail(TPL_ERR_INPUT, msg_input("Input vector `b` must not be a zero vector."));
+    if (d.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
     if (d.steps == 0) { // :64-66
       zero_out(op, x_out, mem);
       return;
@@ -1477,53 +1484,61 @@ tpl_status tpl_op_tune_order(tpl_op_t op, const int32_t* groups, int32_t count, 
     const int32_t cnt = count > 0 ? count : (int32_t)(sizeof(kDefault) / sizeof(kDefault[0]));
     for (int32_t i = 0; i < cnt; ++i)
       if (list[i] <= 0) fail(TPL_ERR_INVALID_ARGUMENT, "group counts must be positive");
-    op->reorder = 1;
-    // any non-zero b: the timed SpMV launches need a step's valid partials and norms
-    const std::vector<double> ones(op->n, 1.0);
-    double best = 0.0;
-    int32_t best_g = op->sp.order_groups;
-    for (int32_t i = 0; i < cnt; ++i) {
-      op->sp.order_groups = list[i];
+    // a failed timing launch leaves the operator as it was (order mode, group count)
+    const int saved_reorder = op->reorder, saved_groups = op->sp.order_groups;
+    try {
+      op->reorder = 1;
+      // any non-zero b: the timed SpMV launches need a step's valid partials and norms
+      // (b is the solver's input staging buffer, re-written by every solve)
+      const std::vector<double> ones(op->n, 1.0);
+      double best = 0.0;
+      int32_t best_g = op->sp.order_groups;
+      for (int32_t i = 0; i < cnt; ++i) {
+        op->sp.order_groups = list[i];
+        rebuild_schedule(op);
+        if (op->perm.empty()) break;  // no long rows: nothing to order
+        if (op->n > 0)
+          HIPCHK(hipMemcpy(op->b, ones.data(), op->n * sizeof(double), hipMemcpyHostToDevice));
+        double t1 = 0.0, t2 = 0.0;
+        for (const auto& kt : {std::make_pair(TPL_KERNEL_PASS1_SPMV, &t1),
+                               std::make_pair(TPL_KERNEL_PASS2_SPMV, &t2)}) {
+          const tpl_status st = tpl_profile_kernel(op, kt.first, iters, kt.second, nullptr);
+          if (st != TPL_OK) fail(st, tpl_last_error());
+        }
+        if (i == 0 || t1 + t2 < best) {
+          best = t1 + t2;
+          best_g = list[i];
+        }
+      }
+      op->sp.order_groups = best_g;
       rebuild_schedule(op);
-      if (op->perm.empty()) break;  // no long rows: nothing to order
-      if (op->n > 0)
-        HIPCHK(hipMemcpy(op->b, ones.data(), op->n * sizeof(double), hipMemcpyHostToDevice));
-      double t1 = 0.0, t2 = 0.0;
-      for (const auto& kt : {std::make_pair(TPL_KERNEL_PASS1_SPMV, &t1),
-                             std::make_pair(TPL_KERNEL_PASS2_SPMV, &t2)}) {
-        const tpl_status st = tpl_profile_kernel(op, kt.first, iters, kt.second, nullptr);
-        if (st != TPL_OK) fail(st, tpl_last_error());
-      }
-      if (i == 0 || t1 + t2 < best) {
-        best = t1 + t2;
-        best_g = list[i];
-      }
+      if (chosen) *chosen = best_g;
+      if (best_us) *best_us = best;
+    } catch (...) {
+      op->reorder = saved_reorder;
+      op->sp.order_groups = saved_groups;
+      hipGetLastError();
+      rebuild_schedule(op);
+      throw;
     }
-    op->sp.order_groups = best_g;
-    rebuild_schedule(op);
-    if (chosen) *chosen = best_g;
-    if (best_us) *best_us = best;
   });
 }
 
-tpl_status tpl_locality_order(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
-                              int32_t short_row_max, int32_t groups, int32_t* perm,
-                              int32_t* applied) {
+tpl_status tpl_op_set_order_groups(tpl_op_t op, int32_t groups) {
   return guarded([&] {
-    if (n < 0 || (n > 0 && (!row_ptr || !perm)) || !applied)
-      fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
-    if (n >= INT32_MAX || (n > 0 && row_ptr[n] >= INT32_MAX))
-      fail(TPL_ERR_UNSUPPORTED, "n and nnz must be < 2^31");
-    std::vector<int32_t> rp(n + 1);
-    for (int64_t i = 0; i <= n; ++i) rp[i] = (int32_t)(n > 0 ? row_ptr[i] : 0);
-    std::vector<int32_t> col(col_idx, col_idx + (n > 0 ? row_ptr[n] : 0));
-    SchedParams sp;
-    sp.short_row_max = short_row_max > 0 ? short_row_max : -1;
-    if (groups > 0) sp.order_groups = groups;
-    const std::vector<int32_t> p = locality_order(n, rp, col, sp);
-    *applied = p.empty() ? 0 : 1;
-    for (int64_t i = 0; i < n; ++i) perm[i] = p.empty() ? (int32_t)i : p[i];
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    if (groups < 0) fail(TPL_ERR_INVALID_ARGUMENT, "group count must be >= 0 (0: default 16)");
+    if (op->dist) fail(TPL_ERR_UNSUPPORTED, "the locality order is single-GPU only");
+    set_device(op);
+    sync_checked(op);
+    op->sp.order_groups = groups > 0 ? groups : SchedParams{}.order_groups;
+    rebuild_schedule(op);
   });
+}
+
+int32_t tpl_op_order_groups(tpl_op_t op) {
+  if (!op) return -1;
+  return op->d_perm ? op->sp.order_groups : 0;
 }
 
 // ------------------------------------------------------------ row partition
@@ -1610,16 +1625,8 @@ tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t*
     const int64_t nnz = row_ptr[n];
     if (row_ptr[0] != 0 || nnz < 0 || nnz >= INT32_MAX)
       fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0; nnz < 2^31");
-    if (nnz > 0 && (!col_idx || !vals)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
-    for (int64_t i = 0; i < n; ++i) {
-      if (row_ptr[i + 1] < row_ptr[i]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
-      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
-        const int32_t c = col_idx[q];
-        if (c < 0 || c >= n_global) fail(TPL_ERR_INVALID_ARGUMENT, "column index out of range");
-        if (q > row_ptr[i] && c <= col_idx[q - 1])
-          fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be strictly ascending per row");
-      }
-    }
+    if (nnz > 0 && !vals) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    check_csr(n, n_global, row_ptr, col_idx);
     HIPCHK(hipSetDevice(d->ctx.device));
     auto op = std::make_unique<tpl_op_s>();
     op->ctx = &d->ctx;
@@ -1650,16 +1657,10 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
     const int64_t nnz = row_ptr[n];
     if (n < 1 || n >= INT32_MAX / 2 || nnz >= INT32_MAX || row_ptr[0] != 0)
       fail(TPL_ERR_INVALID_ARGUMENT, "bad CSR sizes");
-    if (nnz > 0 && (!col_idx || !vals)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    if (nnz > 0 && !vals) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    check_csr(n, n, row_ptr, col_idx);
     std::vector<int32_t> rp32(n + 1);
-    for (int64_t i = 0; i <= n; ++i) {
-      if (i > 0 && row_ptr[i] < row_ptr[i - 1]) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr not monotone");
-      rp32[i] = (int32_t)row_ptr[i];
-    }
-    for (int64_t i = 0; i < n; ++i)
-      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q)
-        if (col_idx[q] < 0 || col_idx[q] >= n || (q > row_ptr[i] && col_idx[q] <= col_idx[q - 1]))
-          fail(TPL_ERR_INVALID_ARGUMENT, "column indices must be in range and ascending per row");
+    for (int64_t i = 0; i <= n; ++i) rp32[i] = (int32_t)row_ptr[i];
     // short / long rows by the global rule; long rows are replicated on every rank
     const int32_t T = short_row_threshold(n, rp32, -1);
     std::vector<int64_t> S, Lr;
@@ -1714,36 +1715,8 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
     // vector is permuted on the device.
     std::vector<int64_t> mine(S.begin() + cut[me], S.begin() + cut[me + 1]);
     if (nl > 0 && op->n <= kReorderAutoMaxRows) {
-      const int32_t gsize = (int32_t)((nl + 15) / 16);
-      struct Key {
-        int32_t tail, glo, ghi, rlo, rhi;
-        int64_t row;
-      };
-      std::vector<Key> keys;
-      keys.reserve(mine.size());
-      for (int64_t i : mine) {
-        int32_t lo = INT32_MAX, hi = INT32_MAX, tail = 0;
-        for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
-          const int32_t r = lidx[col_idx[q]];
-          if (r < 0) {
-            tail |= col_idx[q] != i;
-            continue;
-          }
-          if (lo == INT32_MAX) lo = r;
-          hi = r;
-        }
-        auto grp = [&](int32_t r) { return r == INT32_MAX ? INT32_MAX : r / gsize; };
-        keys.push_back(Key{tail, grp(lo), grp(hi), lo, hi, i});
-      }
-      std::sort(keys.begin(), keys.end(), [](const Key& x, const Key& y) {
-        if (x.tail != y.tail) return x.tail < y.tail;
-        if (x.glo != y.glo) return x.glo < y.glo;
-        if (x.ghi != y.ghi) return x.ghi < y.ghi;
-        if (x.rlo != y.rlo) return x.rlo < y.rlo;
-        if (x.rhi != y.rhi) return x.rhi < y.rhi;
-        return x.row < y.row;
-      });
-      for (size_t p = 0; p < keys.size(); ++p) mine[p] = keys[p].row;
+      // lidx is each long row's rank among the long rows, as locality_order ranks them
+      locality_sort(mine, row_ptr, col_idx, lidx.data(), (int32_t)nl, op->sp.order_groups);
       op->local_order = true;
     }
     op->g2l.assign(n, -1);

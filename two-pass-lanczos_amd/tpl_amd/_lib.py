@@ -126,6 +126,19 @@ tpl_locality_order = _sig("tpl_locality_order", c_int, c_int64, POINTER(c_int64)
                           POINTER(c_int32), c_int32, c_int32, POINTER(c_int32),
                           POINTER(c_int32))
 tpl_op_reorth_second_passes = _sig("tpl_op_reorth_second_passes", c_int, c_void_p, POINTER(c_int64))
+tpl_op_set_order_groups = _sig("tpl_op_set_order_groups", c_int, c_void_p, c_int32)
+tpl_op_order_groups = _sig("tpl_op_order_groups", c_int32, c_void_p)
+
+
+class ErrorDetail(ctypes.Structure):
+    """tpl_error_detail: the fields of the last failing call's LanczosErrorKind."""
+    _fields_ = [("status", c_int32), ("message", c_char_p), ("inner", c_char_p),
+                ("param_name", c_char_p), ("expected", ctypes.c_uint64),
+                ("actual", ctypes.c_uint64), ("operator_cols", ctypes.c_uint64),
+                ("vector_rows", ctypes.c_uint64), ("breakdown_step", ctypes.c_uint64)]
+
+
+tpl_last_error_detail = _sig("tpl_last_error_detail", c_int, POINTER(ErrorDetail))
 
 # built-in f(T_k) solvers: raw C function pointers usable as tpl_ftk_fn
 FTK_INV_PTR = ctypes.cast(lib.tpl_ftk_inv, c_void_p).value
@@ -150,12 +163,25 @@ EXPORTED = [
     "tpl_op_set_value_format", "tpl_op_set_device_ftk",
     "tpl_op_device_bytes", "tpl_op_reorth_second_passes", "tpl_op_set_reorder",
     "tpl_op_permutation", "tpl_locality_order", "tpl_op_tune_order",
+    "tpl_last_error_detail", "tpl_op_set_order_groups", "tpl_op_order_groups",
 ]
 
 
 def last_error() -> str:
     m = tpl_last_error()
     return m.decode("utf-8", "replace") if m else ""
+
+
+def last_error_detail() -> dict:
+    """tpl_last_error_detail as a dict (strings decoded)."""
+    d = ErrorDetail()
+    if tpl_last_error_detail(ctypes.byref(d)) != TPL_OK:
+        raise RuntimeError("tpl_last_error_detail failed")
+    dec = (lambda b: b.decode("utf-8", "replace") if b else "")
+    return {"status": d.status, "message": dec(d.message), "inner": dec(d.inner),
+            "param_name": dec(d.param_name), "expected": int(d.expected),
+            "actual": int(d.actual), "operator_cols": int(d.operator_cols),
+            "vector_rows": int(d.vector_rows), "breakdown_step": int(d.breakdown_step)}
 
 # row-partitioned operator (include/tpl.h, "row-partitioned operator over several GPUs")
 TPL_DIST_ID_BYTES = 128

@@ -96,13 +96,36 @@ _KIND_OF_STATUS = {
 }
 
 
+def from_detail(d: dict) -> "LanczosError":
+    """Rebuild the LanczosErrorKind variant from tpl_last_error_detail's fields (not by
+    parsing the message): the same constructors a Rust binding uses."""
+    st = d["status"]
+    if st == _lib.TPL_ERR_INPUT:
+        return LanczosError.input_error(d["inner"])
+    if st == _lib.TPL_ERR_PARAMETER_MISMATCH:
+        return LanczosError.parameter_mismatch(d["param_name"], d["expected"], d["actual"])
+    if st == _lib.TPL_ERR_DIMENSION_MISMATCH:
+        return LanczosError.dimension_mismatch(d["operator_cols"], d["vector_rows"])
+    if st == _lib.TPL_ERR_SOLVER:
+        return LanczosError.solver_error(d["inner"])
+    if st == _lib.TPL_ERR_EVD:
+        return LanczosError.evd_error(d["inner"])
+    if st == _lib.TPL_ERR_BREAKDOWN:
+        return LanczosError.breakdown(d["breakdown_step"])
+    raise ValueError(f"status {st} is not a LanczosErrorKind")
+
+
 def check(status: int) -> None:
     """Raise the Python mirror of a non-zero tpl_status."""
     if status == _lib.TPL_OK:
         return
     msg = _lib.last_error()
     if status in _KIND_OF_STATUS:
-        raise LanczosError(_KIND_OF_STATUS[status], msg)
+        err = from_detail(_lib.last_error_detail())
+        if err.message != msg:  # the fields must reproduce the engine's Display text
+            raise TplError(_lib.TPL_ERR_INVALID_ARGUMENT,
+                           f"error detail does not match the message: {err.message!r} != {msg!r}")
+        raise err
     if status == _lib.TPL_ERR_DATA_LOADER:
         raise DataLoaderError(msg)
     raise TplError(status, msg)

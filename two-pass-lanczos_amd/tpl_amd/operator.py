@@ -167,6 +167,15 @@ class HipCsrOp:
                                      int(g.size), int(iters), byref(chosen), byref(us)))
         return int(chosen.value), float(us.value)
 
+    def set_order_groups(self, groups: int = 0):
+        """Pin the locality order's group count (0: the default 16); deterministic, unlike
+        tune_order (tpl_op_set_order_groups)."""
+        check(_lib.tpl_op_set_order_groups(self._op, int(groups)))
+
+    def order_groups(self) -> int:
+        """Group count of the order the device holds (0: the caller's order)."""
+        return int(_lib.tpl_op_order_groups(self._op))
+
     def set_reorder(self, mode=2):
         """Locality row order on the device (rebuilds the layout): False / 0 off,
         True / 1 on, 2 auto (default: on up to 2^20 rows). The caller's row order is
