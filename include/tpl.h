@@ -201,11 +201,23 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k,
  * On an error x_out is unspecified.                                               */
 tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                                 tpl_ftk_fn f, void* f_user, double* x_out, int mem);
-/* Where tpl_lanczos_two_pass evaluates the built-in inv: mode 0 = host (two graphs),
- * 1 = device for k <= 1365 (one graph), 2 = auto (default): device for k <= 128, where
- * the single-lane device solve (a chain of ~2k divisions) costs no more than the host
- * round trip it removes.                                                          */
+/* Where tpl_lanczos_two_pass evaluates the built-in f(T_k): mode 0 = host (two graphs
+ * around the host call), 1 = device (the whole solve one graph), 2 = auto (default).
+ *   inv: device for k <= 1365 (mode 1) / k <= 128 (auto: the single-lane device solve,
+ *        a chain of ~2k divisions with the host solver's exact operations, costs no more
+ *        than the host round trip it removes there); bitwise the host result.
+ *   exp: device for k <= 1800 (modes 1 and 2): a Chebyshev expansion of exp over the
+ *        Sturm-bracketed spectrum, parallel over the rows of T_k, within
+ *        a small multiple of eps * exp(lambda_max) of the host QL result — the accuracy
+ *        class of the reference's EVD (src/bin/stability.rs:175-193), not its bits. A
+ *        T_k that is not finite or whose spectrum is too wide for the expansion is handed
+ *        back to the host solver inside the same call.                              */
 tpl_status tpl_op_set_device_ftk(tpl_op_t op, int mode);
+/* Test / introspection: evaluate the device f(T_k) kernel alone on a given T_k (which 0:
+ * inv, 1: exp; n alphas, n - 1 betas) into y_out (n host doubles, y' = f(T_k) e_1).
+ * *on_device = 0 when the exp kernel handed the case back to the host (y_out then 0).  */
+tpl_status tpl_op_ftk_device(tpl_op_t op, int which, const double* alphas, size_t n,
+                             const double* betas, double* y_out, int* on_device);
 
 /* ---- low-level API: src/algorithms/ -------------------------------------- */
 /* Per-step callback of lanczos_standard (LanczosCallback, src/algorithms/mod.rs:82-86):

@@ -62,3 +62,89 @@ def sq(alphas, betas) -> np.ndarray:
 
 
 SOLVERS = {"inv": inv, "exp": exp, "sq": sq}
+
+
+def exp_chebyshev(alphas, betas, rounds: int = 2, shifts: int = 128) -> np.ndarray:
+    """Restatement of the device exp (two-pass-lanczos_amd/csrc/tpl_kernels.hip k_ftk_exp)
+    in numpy — TEST INFRASTRUCTURE: it checks the algorithm (Sturm multisection bracket,
+    Debye-sized Chebyshev expansion, Clenshaw + Miller's backward Bessel recurrence)
+    against LAPACK on the CPU; the device's bits are not reproduced (libm exp/asinh differ).
+    Returns y' = exp(T) e_1, or None where the device hands the case back to the host."""
+    al = np.asarray(alphas, dtype=np.float64)
+    n = len(al)
+    be = np.zeros(n)
+    be[:n - 1] = np.asarray(betas[:n - 1], dtype=np.float64)
+    if not (np.all(np.isfinite(al)) and np.all(np.isfinite(be))):
+        return None
+    if n == 1:
+        return np.array([np.exp(al[0])])
+    bl = np.concatenate([[0.0], be[:n - 1]])
+    rad = np.abs(bl) + np.abs(be)
+    glo, ghi = float(np.min(al - rad)), float(np.max(al + rad))
+    pivmin = 2.2250738585072014e-308 * max(1.0, float(np.max(be * be)))
+
+    def count(sig):
+        q = al[0] - sig
+        if abs(q) < pivmin:
+            q = -pivmin
+        c = int(q < 0)
+        for i in range(1, n):
+            q = (al[i] - sig) - (be[i - 1] * be[i - 1]) / q
+            if abs(q) < pivmin:
+                q = -pivmin
+            c += int(q < 0)
+        return c
+
+    brk = [glo, ghi, glo, ghi]
+    for _ in range(rounds):
+        for end in (0, 1):
+            L, U = brk[2 * end], brk[2 * end + 1]
+            need = n if end else 1
+            sig = [L + (U - L) * ((q + 1) / (shifts + 1)) for q in range(shifts)]
+            j = next((q for q in range(shifts) if count(sig[q]) >= need), shifts)
+            brk[2 * end] = L + (U - L) * (j / (shifts + 1)) if j > 0 else L
+            brk[2 * end + 1] = sig[j] if j < shifts else U
+    scale = max(abs(glo), abs(ghi))
+    a = brk[0] - 1e-9 * (1.0 + scale)
+    b = brk[3] + 1e-9 * (1.0 + scale)
+    c = 0.5 * (a + b)
+    r = max(0.5 * (b - a), 1e-30 * (1.0 + abs(c)))
+
+    def lsi(m):
+        s = np.sqrt(m * m + r * r)
+        return -r + s - m * np.arcsinh(m / r) - 0.9189385332046727 - 0.25 * np.log(s * s)
+
+    lo_m, hi_m = 0, 16384
+    if lsi(hi_m) >= -50.66:
+        return None
+    while lo_m < hi_m:
+        mid = (lo_m + hi_m) >> 1
+        if lsi(mid) < -50.66:
+            hi_m = mid
+        else:
+            lo_m = mid + 1
+    N = lo_m + 8
+
+    def xprod(v):
+        out = (al - c) * v
+        out[1:] += be[:n - 1] * v[:n - 1]
+        out[:n - 1] += be[:n - 1] * v[1:]
+        return out / r
+
+    b1, b2 = np.zeros(n), np.zeros(n)
+    ip1, im, ssum = 0.0, 1.0, 0.0
+    for m in range(N, 0, -1):
+        v = 2.0 * xprod(b1) - b2
+        v[0] += 2.0 * im
+        b2, b1 = b1, v
+        ssum += 2.0 * im
+        ip1, im = im, ip1 + (2.0 * m / r) * im
+        if abs(im) > 1e200:
+            im, ip1, ssum = im * 1e-200, ip1 * 1e-200, ssum * 1e-200
+            b1, b2 = b1 * 1e-200, b2 * 1e-200
+    v = xprod(b1) - b2
+    v[0] += im
+    yv = v / (ssum + im)
+    if not np.sum(yv * yv) >= 1e-6:  # ||exp(T - bI) e_1|| < 1e-3: handed to the host
+        return None
+    return np.exp(b) * yv

@@ -108,7 +108,9 @@ def test_auto_mode(kkt5k):
     assert op.flags() & ONE_GRAPH
     solvers.lanczos_two_pass(op, b, 129, ftk.INV)
     assert not op.flags() & ONE_GRAPH
-    solvers.lanczos_two_pass(op, b, 50, ftk.EXP)  # a host f is never moved to the device
+    solvers.lanczos_two_pass(op, b, 50, ftk.EXP)  # the built-in exp: on the device too
+    assert op.flags() & ONE_GRAPH
+    solvers.lanczos_two_pass(op, b, 50, lambda al, be: ftk.EXP(al, be))  # a host f stays
     assert not op.flags() & ONE_GRAPH
     with pytest.raises(tpl_amd.TplError):
         op.set_device_ftk(3)

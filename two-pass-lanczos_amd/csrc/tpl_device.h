@@ -150,8 +150,10 @@ struct CsrDev {
 };
 
 // Device-resident solver state (one per operator).
+constexpr int kFlagBytes = 32;       // DevState::flags: 8 int32
 struct DevState {
-  int32_t* flags;   // [0] stop, [1] error (1 = zero b), [2] steps_taken
+  int32_t* flags;   // [0] stop, [1] error (1 = zero b), [2] steps_taken, [3] second
+                    // Gram-Schmidt passes, [4] device f(T_k) handed back to the host
   double* norms;    // [0] = ||b||, [j] = beta_j                         (kcap+1)
   double* alphas;   // alphas[j-1] = alpha_j                              (kcap)
   double* betas;    // betas[j-1]  = beta_j                               (kcap)

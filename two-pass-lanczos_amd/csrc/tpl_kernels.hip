@@ -49,6 +49,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
     S.flags[1] = 0;
     S.flags[2] = 0;
     S.flags[3] = 0;
+    S.flags[4] = 0;
   }
   const int rb = elem_block(A, blockIdx.x);
   if (rb < 0) return;
@@ -369,6 +370,241 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
       x1 = x0;
       x0 = xi;
     }
+  }
+}
+
+// f(T_k) = exp(T_k) on the device: y = ||b|| exp(T_k) e_1 (src/bin/stability.rs:175-193
+// forms Q exp(Lambda) Q^T e_1 from a dense EVD; the host built-in tpl_ftk_exp runs QL).
+// A QL sweep is one long chain of dependent rotations (1.2 ms at k = 200 on the host, worse
+// on one GPU lane), so the device evaluates the same function with a parallel method: the
+// Chebyshev expansion of exp on an interval [a, b] holding the spectrum,
+//   exp(c + r x) = e^c (I_0(r) + 2 sum_m I_m(r) T_m(x)),  c = (a+b)/2, r = (b-a)/2,
+// applied to e_1 with x = (T - c)/r by Clenshaw's recurrence (every row of the tridiagonal
+// product on its own thread, one LDS exchange and barrier per term), the modified Bessel
+// coefficients generated alongside by Miller's backward recurrence I_{m-1} = I_{m+1} +
+// (2m/r) I_m and normalised by e^r = I_0 + 2 sum I_m — no coefficient table, no EVD, and
+// no clusters to resolve (eigenvectors never appear). [a, b]: two rounds of 128-way Sturm
+// multisection per end from the Gershgorin bounds (a count is exact for a matrix within a
+// few ulps of T, so the bracket holds the spectrum up to the added margin). Accuracy is the
+// EVD's class: the error is a small multiple of eps * exp(lambda_max) (the coefficients sum
+// to e^b), against the tolerance the host QL itself meets; the terms run until the
+// coefficients fall below 1e-22 of e^b (Debye asymptotics of I_m(r)). Falls back to the host
+// (flags[4] = 1, y = 0) when T is not finite, when the expansion needs more than
+// kExpMaxTerms terms (|lambda_max - lambda_min| above ~2e4), or when ||y|| < 1e-3 e^b
+// (the absolute error bound would not be small against ||y||). Dynamic LDS: 4 kcap + 4 doubles
+// and 256 ints.
+constexpr int kExpRows = 8;          // rows per thread: n <= 2048 (the LDS bound is lower)
+constexpr int kExpMaxTerms = 16384;
+constexpr double kExpMinRatio = 1e-3;  // ||exp(T - b I) e_1|| below this: host (see the end)
+__device__ __forceinline__ int sturm_count(const double* al, const double* be, int n,
+                                           double sigma, double pivmin) {
+  double q = al[0] - sigma;
+  if (fabs(q) < pivmin) q = -pivmin;
+  int cnt = q < 0.0;
+  for (int i = 1; i < n; ++i) {
+    const double b = be[i - 1];
+    q = (al[i] - sigma) - (b * b) / q;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+  }
+  return cnt;
+}
+// ln(e^-r I_m(r)), uniform asymptotic (Debye) form; used only to size the expansion
+__device__ __forceinline__ double log_scaled_bessel_i(double m, double r) {
+  const double s = sqrt(m * m + r * r);
+  return -r + s - m * asinh(m / r) - 0.9189385332046727 - 0.25 * log(s * s);
+}
+__global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
+  extern __shared__ double sh[];
+  __shared__ double red[2][kTPB];
+  __shared__ int cnt[kTPB];
+  __shared__ double brk[4];  // [lo_L, lo_U, hi_L, hi_U]
+  const int n = S.flags[2];
+  if (S.flags[1] || n < 1) return;
+  const int t = threadIdx.x;
+  double* al = sh;            // alpha (n)
+  double* be = sh + n;        // beta (n - 1), be[n-1] = 0
+  double* buf0 = sh + 2 * n;  // Clenshaw exchange buffers: row i at [i + 1], zeros at both ends
+  double* buf1 = buf0 + (n + 2);
+  const double bnorm = S.norms[0];
+  // load; Gershgorin bounds, largest beta^2, finiteness
+  double glo = INFINITY, ghi = -INFINITY, bmax = 0.0;
+  bool finite = true;
+  for (int i = t; i < n; i += kTPB) {
+    const double a = S.alphas[i];
+    const double bl = i > 0 ? S.betas[i - 1] : 0.0, br = i + 1 < n ? S.betas[i] : 0.0;
+    al[i] = a;
+    be[i] = br;
+    finite = finite && isfinite(a) && isfinite(br);
+    const double rad = fabs(bl) + fabs(br);
+    glo = fmin(glo, a - rad);
+    ghi = fmax(ghi, a + rad);
+    bmax = fmax(bmax, br * br);
+  }
+  for (int i = t; i < n + 2; i += kTPB) buf0[i] = buf1[i] = 0.0;
+  red[0][t] = glo;
+  red[1][t] = ghi;
+  cnt[t] = finite ? 0 : 1;
+  __syncthreads();
+  for (int h = kTPB / 2; h > 0; h >>= 1) {
+    if (t < h) {
+      red[0][t] = fmin(red[0][t], red[0][t + h]);
+      red[1][t] = fmax(red[1][t], red[1][t + h]);
+      cnt[t] |= cnt[t + h];
+    }
+    __syncthreads();
+  }
+  glo = red[0][0];
+  ghi = red[1][0];
+  const bool bad = cnt[0] != 0;
+  __syncthreads();
+  red[0][t] = bmax;
+  __syncthreads();
+  for (int h = kTPB / 2; h > 0; h >>= 1) {
+    if (t < h) red[0][t] = fmax(red[0][t], red[0][t + h]);
+    __syncthreads();
+  }
+  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, red[0][0]);
+  auto fallback = [&]() {
+    for (int i = t; i < n; i += kTPB) S.y[i] = 0.0;
+    if (t == 0) S.flags[4] = 1;
+  };
+  if (bad) {
+    fallback();
+    return;
+  }
+  if (n == 1) {
+    if (t == 0) S.y[0] = exp(al[0]) * bnorm;
+    return;
+  }
+  // two rounds of 128-way Sturm multisection per end: threads 0..127 bracket lambda_min
+  // (first shift with a count >= 1), threads 128..255 lambda_max (first count == n)
+  if (t == 0) {
+    brk[0] = glo; brk[1] = ghi; brk[2] = glo; brk[3] = ghi;
+  }
+  __syncthreads();
+  constexpr int P = kTPB / 2;
+  const bool hi_end = t >= P;
+  const int tt = hi_end ? t - P : t;
+  for (int round = 0; round < 2; ++round) {
+    const double L = brk[hi_end ? 2 : 0], U = brk[hi_end ? 3 : 1];
+    const double sigma = L + (U - L) * ((double)(tt + 1) / (double)(P + 1));
+    cnt[t] = sturm_count(al, be, n, sigma, pivmin);
+    __syncthreads();
+    if (t == 0 || t == P) {
+      const int need = hi_end ? n : 1;
+      int j = 0;
+      while (j < P && cnt[t + j] < need) ++j;
+      const double s_at = [&](int q) { return L + (U - L) * ((double)(q + 1) / (double)(P + 1)); }(j);
+      const double nl = j > 0 ? L + (U - L) * ((double)j / (double)(P + 1)) : L;
+      brk[hi_end ? 2 : 0] = nl;
+      brk[hi_end ? 3 : 1] = j < P ? s_at : U;
+    }
+    __syncthreads();
+  }
+  // [a, b] holds the spectrum: the lower end of lambda_min's bracket, the upper end of
+  // lambda_max's, widened by a margin far above a Sturm count's backward error
+  const double scale = fmax(fabs(glo), fabs(ghi));
+  const double a = brk[0] - 1e-9 * (1.0 + scale);
+  const double b = brk[3] + 1e-9 * (1.0 + scale);
+  const double c = 0.5 * (a + b);
+  const double r = fmax(0.5 * (b - a), 1e-30 * (1.0 + fabs(c)));
+  const double inv_r = 1.0 / r;
+  // terms: the smallest m with e^-r I_m(r) < 1e-22 (binary search on the asymptotic form),
+  // plus a margin for Miller's start
+  int lo_m = 0, hi_m = kExpMaxTerms;
+  if (log_scaled_bessel_i((double)hi_m, r) >= -50.66) {
+    fallback();
+    return;
+  }
+  while (lo_m < hi_m) {
+    const int mid = (lo_m + hi_m) >> 1;
+    if (log_scaled_bessel_i((double)mid, r) < -50.66) hi_m = mid; else lo_m = mid + 1;
+  }
+  const int N = lo_m + 8;
+  // Clenshaw: b_m = a_m e_1 + 2 x b_{m+1} - b_{m+2} (m = N .. 1), x = (T - c I) / r; the
+  // result is a_0 e_1 + x b_1 - b_2 with a_0 = I_0, a_m = 2 I_m (unnormalised Miller values)
+  const int R = (n + kTPB - 1) / kTPB;
+  double b1[kExpRows], b2[kExpRows];
+#pragma unroll
+  for (int u = 0; u < kExpRows; ++u) b1[u] = b2[u] = 0.0;
+  double Ip1 = 0.0, Im = 1.0, Ssum = 0.0;  // I_{m+1}, I_m (Miller seed), 2 sum_{m'>=m} I_m'
+  double* cur = buf0;
+  double* nxt = buf1;
+  auto xprod = [&](const double* v, int i) {  // (x v)_i, v stored at [i + 1]
+    return ((be[i > 0 ? i - 1 : 0] * (i > 0 ? v[i] : 0.0) + (al[i] - c) * v[i + 1]) +
+            be[i] * v[i + 2]) * inv_r;
+  };
+  for (int m = N; m >= 1; --m) {
+    // publish b_{m+1}, then every row forms b_m from its neighbours
+#pragma unroll
+    for (int u = 0; u < kExpRows; ++u) {
+      const int i = t + u * kTPB;
+      if (u < R && i < n) cur[i + 1] = b1[u];
+    }
+    __syncthreads();
+    const double am = 2.0 * Im;
+#pragma unroll
+    for (int u = 0; u < kExpRows; ++u) {
+      const int i = t + u * kTPB;
+      if (u < R && i < n) {
+        double v = 2.0 * xprod(cur, i) - b2[u];
+        if (i == 0) v = v + am;
+        b2[u] = b1[u];
+        b1[u] = v;
+      }
+    }
+    Ssum = Ssum + am;
+    const double Inext = Ip1 + (2.0 * (double)m * inv_r) * Im;
+    Ip1 = Im;
+    Im = Inext;
+    if (fabs(Im) > 1e200) {  // Miller's values grow towards m = 0: rescale the whole state
+      Im *= 1e-200; Ip1 *= 1e-200; Ssum *= 1e-200;
+#pragma unroll
+      for (int u = 0; u < kExpRows; ++u) { b1[u] *= 1e-200; b2[u] *= 1e-200; }
+    }
+    double* sw = cur; cur = nxt; nxt = sw;  // double buffer: one barrier per term
+  }
+  // y' = e^b (I_0 e_1 + x b_1 - b_2) / (I_0 + 2 sum I_m)
+#pragma unroll
+  for (int u = 0; u < kExpRows; ++u) {
+    const int i = t + u * kTPB;
+    if (u < R && i < n) cur[i + 1] = b1[u];
+  }
+  __syncthreads();
+  const double norm = Ssum + Im;
+  const double eb = exp(b);
+  double yv[kExpRows];
+  double sq = 0.0;
+#pragma unroll
+  for (int u = 0; u < kExpRows; ++u) {
+    const int i = t + u * kTPB;
+    yv[u] = 0.0;
+    if (u < R && i < n) {
+      double v = xprod(cur, i) - b2[u];
+      if (i == 0) v = v + Im;
+      yv[u] = v / norm;  // exp(T - b I) e_1
+      sq = fma(yv[u], yv[u], sq);
+    }
+  }
+  // The expansion's error is a few eps * (terms) in units of e^b; when ||exp(T - bI) e_1||
+  // is far below 1 (e_1 nearly orthogonal to the top of the spectrum) that is no longer
+  // small against ||y||, while the EVD keeps its relative accuracy: hand such cases back.
+  __syncthreads();
+  red[0][t] = sq;
+  __syncthreads();
+  for (int h = kTPB / 2; h > 0; h >>= 1) {
+    if (t < h) red[0][t] = red[0][t] + red[0][t + h];
+    __syncthreads();
+  }
+  if (!(red[0][0] >= kExpMinRatio * kExpMinRatio)) {
+    fallback();
+    return;
+  }
+#pragma unroll
+  for (int u = 0; u < kExpRows; ++u) {
+    const int i = t + u * kTPB;
+    if (u < R && i < n) S.y[i] = (eb * yv[u]) * bnorm;
   }
 }
 
@@ -705,6 +941,10 @@ hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], 
 }
 hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s) {
   hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)6 * kcap * sizeof(double), s, S);
+  return hipGetLastError();
+}
+hipError_t ftk_exp(const DevState& S, int kcap, hipStream_t s) {
+  hipLaunchKernelGGL(k_ftk_exp, dim3(1), dim3(kTPB), (size_t)(4 * kcap + 4) * sizeof(double), s, S);
   return hipGetLastError();
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,

@@ -38,6 +38,7 @@ hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], 
 hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
                    const int32_t* idx, hipStream_t s);
 hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s);
+hipError_t ftk_exp(const DevState& S, int kcap, hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, int dyn, hipStream_t s);
 // nflush: x terms the step applies (tpl::p2_flush: every third step and the last)
@@ -124,6 +125,11 @@ constexpr size_t kDevFtkMaxK = 1365;
 // (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
 // ~15-25 us (sync, host solve, upload, launch): one graph pays up to k ~ 128.
 constexpr size_t kDevFtkAutoK = 128;
+// The device exp (k_ftk_exp, a Chebyshev expansion: parallel over the rows of T_k) keeps 4 k
+// doubles in LDS (with its static arrays, under 64 KiB up to this k).
+constexpr size_t kDevExpMaxK = 1800;
+// Which built-in f(T_k) a one-graph solve evaluates on the device.
+enum DevF { kDevInv = 0, kDevExp = 1 };
 // Locality order, auto mode: on up to this many rows. Measured k_p2_spmv (KKT, D = 0;
 // profiles/r02_order_lab.txt): 500k arcs 8.76 -> 6.91 us, 1M arcs 12.8 -> 11.8 us,
 // 50k / 5k arcs flat; 2M arcs 20.5 -> 21.8 us and 5M arcs 54 -> 58 us (the gathered
@@ -355,7 +361,7 @@ void rebuild_schedule(tpl_op_s* op) {
   op->kcap = 0;
 }
 
-// state layout: [flags: 4 int32 (16 B)] [norms kcap+1] [alphas kcap] [betas kcap] [y kcap] [Pa G] [Pb G] [Pr G*kcap]
+// state layout: [flags: 8 int32 (kFlagBytes)] [norms kcap+1] [alphas kcap] [betas kcap] [y kcap] [Pa G] [Pb G] [Pr G*kcap]
 void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
   if (k > op->kcap) {
     const size_t kc = std::max<size_t>(k, 16);
@@ -368,13 +374,14 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->d_Pr = nullptr;
     const CsrDev A = csr_dev(op);
     const size_t doubles = (kc + 1) + 3 * kc + (size_t)std::max(A.NA, 1) + (size_t)A.G2;
-    const size_t bytes = 16 + doubles * sizeof(double);
+    const size_t bytes = kFlagBytes + doubles * sizeof(double);
     dev_alloc(op, &op->d_state, bytes);
     HIPCHK(hipMemset(op->d_state, 0, bytes));
-    HIPCHK(hipHostMalloc(&op->h_state, 16 + (4 * kc + 1) * sizeof(double), hipHostMallocDefault));
+    HIPCHK(hipHostMalloc(&op->h_state, kFlagBytes + (4 * kc + 1) * sizeof(double),
+                         hipHostMallocDefault));
     char* base = (char*)op->d_state;
     op->S.flags = (int32_t*)base;
-    op->S.norms = (double*)(base + 16);
+    op->S.norms = (double*)(base + kFlagBytes);
     op->S.alphas = op->S.norms + (kc + 1);
     op->S.betas = op->S.alphas + kc;
     op->S.y = op->S.betas + kc;
@@ -639,8 +646,11 @@ void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
 // beta (bitwise the host solver's result); pass two is the k - 1 step launches, those at
 // or past steps_taken doing nothing, with x flushed at multiples of 3 only and the
 // pending terms of the last step added by k_p2_tail (the same sums as the host schedule).
-void enqueue_ftk_dev(tpl_op_s* op, size_t k) {
-  HIPCHK(launch::ftk_inv(op->S, (int)k, op->stream));
+void enqueue_ftk_dev(tpl_op_s* op, size_t k, int f) {
+  if (f == kDevExp)
+    HIPCHK(launch::ftk_exp(op->S, (int)k, op->stream));
+  else
+    HIPCHK(launch::ftk_inv(op->S, (int)k, op->stream));
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, nullptr, 1, op->stream));
 }
 void enqueue_pass2_dyn_steps(tpl_op_s* op, size_t k) {
@@ -707,7 +717,7 @@ void run_pass2(tpl_op_s* op, size_t steps) {
 }
 
 struct HostDecomp {
-  int32_t flags[4];
+  int32_t flags[kFlagBytes / 4];
   double b_norm;
   const double* alphas;
   const double* betas;
@@ -720,13 +730,13 @@ void sync_checked(tpl_op_s* op) { HIPCHK(hipStreamSynchronize(op->stream)); }
 HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
   const size_t kc = op->kcap;
   char* h = (char*)op->h_state;
-  const size_t bytes = 16 + ((kc + 1) + 2 * kc) * sizeof(double);
+  const size_t bytes = kFlagBytes + ((kc + 1) + 2 * kc) * sizeof(double);
   (void)k;
   HIPCHK(hipMemcpyAsync(h, op->d_state, bytes, hipMemcpyDeviceToHost, op->stream));
   sync_checked(op);
   HostDecomp d;
-  std::memcpy(d.flags, h, 16);
-  const double* norms = (const double*)(h + 16);
+  std::memcpy(d.flags, h, kFlagBytes);
+  const double* norms = (const double*)(h + kFlagBytes);
   d.b_norm = norms[0];
   d.alphas = norms + (kc + 1);
   d.betas = d.alphas + kc;
@@ -736,11 +746,12 @@ HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
 
 // The whole two-pass solve as one graph (or, with live timing on, as three graphs with
 // the events between them); no host round trip between the passes.
-void run_two_pass_dev(tpl_op_s* op, size_t k) {
+void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
+  const size_t key = 2 * k + (size_t)f;  // one graph per (k, f)
   if (!op->timing) {
-    run_graph(op, kGTwoPassDev, k, [&] {
+    run_graph(op, kGTwoPassDev, key, [&] {
       enqueue_pass1(op, k, false, false);
-      enqueue_ftk_dev(op, k);
+      enqueue_ftk_dev(op, k, f);
       enqueue_pass2_dyn_steps(op, k);
       enqueue_pass2_tail(op);
     });
@@ -749,7 +760,7 @@ void run_two_pass_dev(tpl_op_s* op, size_t k) {
   HIPCHK(hipEventRecord(op->tev[0], op->stream));
   run_graph(op, kGPass1, k, [&] { enqueue_pass1(op, k, false, false); });
   HIPCHK(hipEventRecord(op->tev[1], op->stream));
-  run_graph(op, kGDevFtk, k, [&] { enqueue_ftk_dev(op, k); });
+  run_graph(op, kGDevFtk, key, [&] { enqueue_ftk_dev(op, k, f); });
   HIPCHK(hipEventRecord(op->tev[2], op->stream));
   run_graph(op, kGPass2Dyn, k, [&] { enqueue_pass2_dyn_steps(op, k); });
   HIPCHK(hipEventRecord(op->tev[3], op->stream));
@@ -1175,26 +1186,42 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
     set_device(op);
     check_b(op, b, b_len);
     check_k(k);
-    const size_t kmax = op->device_ftk == 1 ? kDevFtkMaxK : op->device_ftk == 2 ? kDevFtkAutoK : 0;
-    if (f == &tpl_ftk_inv && !op->dist && k <= kmax) {
-      // one graph: pass one, y = ||b|| T^{-1} e_1 on the device, pass two (the built-in
-      // inv is the same computation as on the host, bit for bit; src/solvers.rs:148-174)
+    // the built-in inv / exp on the device: the whole solve one graph (pass one, f(T_k)
+    // from the device alpha / beta, pass two), no host round trip between the passes
+    const bool is_inv = f == &tpl_ftk_inv, is_exp = f == &tpl_ftk_exp;
+    const size_t kmax = !op->device_ftk ? 0
+                        : is_inv ? (op->device_ftk == 1 ? kDevFtkMaxK : kDevFtkAutoK)
+                        : is_exp ? kDevExpMaxK : 0;
+    bool have_p1 = false;  // pass one already ran (the device handed f back to the host)
+    if ((is_inv || is_exp) && !op->dist && k <= kmax) {
+      // inv: the host solver's operations in its order, bit for bit (src/solvers.rs:148-174);
+      // exp: a parallel evaluation of the same function (k_ftk_exp), EVD-class accuracy
       ensure_state(op, k);
       upload_vec(op, op->b, b, mem);
-      op->last_one_graph = true;
-      run_two_pass_dev(op, k);
+      run_two_pass_dev(op, k, is_exp ? kDevExp : kDevInv);
       download_vec(op, x_out, op->x, 1, mem);
-      HIPCHK(hipMemcpyAsync(op->h_state, op->d_state, 16, hipMemcpyDeviceToHost, op->stream));
+      HIPCHK(hipMemcpyAsync(op->h_state, op->d_state, kFlagBytes, hipMemcpyDeviceToHost,
+                            op->stream));
       sync_checked(op);
-      int32_t flags[4];
-      std::memcpy(flags, op->h_state, 16);
+      int32_t flags[kFlagBytes / 4];
+      std::memcpy(flags, op->h_state, kFlagBytes);
       if (flags[1]) fail_input("Input vector `b` must not be a zero vector.");
-      if (flags[2] == 0) zero_out(op, x_out, mem);
-      return;
+      if (flags[2] == 0) {
+        op->last_one_graph = true;
+        zero_out(op, x_out, mem);
+        return;
+      }
+      if (!flags[4]) {
+        op->last_one_graph = true;
+        return;
+      }
+      // the device handed f(T_k) back (T_k not finite, or a spectrum too wide for the
+      // expansion): the host solver on the same decomposition, then pass two again
+      have_p1 = true;
     }
     // 1. pass one (src/solvers.rs:148)
     op->last_one_graph = false;
-    run_pass_one(op, b, k, mem, false, false);
+    if (!have_p1) run_pass_one(op, b, k, mem, false, false);
     const HostDecomp d = fetch_decomp(op, k);
     if (d.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
     if (d.steps == 0) { // :150-152
@@ -1341,6 +1368,35 @@ tpl_status tpl_op_set_device_ftk(tpl_op_t op, int mode) {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     if (mode < 0 || mode > 2) fail(TPL_ERR_INVALID_ARGUMENT, "device f(T_k) mode must be 0, 1 or 2");
     op->device_ftk = mode;
+  });
+}
+
+tpl_status tpl_op_ftk_device(tpl_op_t op, int which, const double* alphas, size_t n,
+                             const double* betas, double* y_out, int* on_device) {
+  return guarded([&] {
+    if (!op || !alphas || !y_out || !on_device || (n > 1 && !betas))
+      fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (which != 0 && which != 1) fail(TPL_ERR_INVALID_ARGUMENT, "which must be 0 (inv) or 1 (exp)");
+    if (n == 0) fail(TPL_ERR_INVALID_ARGUMENT, "n must be >= 1");
+    if (n > (which == 0 ? kDevFtkMaxK : kDevExpMaxK))
+      fail(TPL_ERR_UNSUPPORTED, "k above the device f(T_k) bound");
+    set_device(op);
+    ensure_state(op, n);
+    // the solver state as pass one leaves it: steps_taken = n, ||b|| = 1, no error
+    int32_t flags[kFlagBytes / 4] = {0, 0, (int32_t)n, 0, 0, 0, 0, 0};
+    const double one = 1.0;
+    HIPCHK(hipMemcpyAsync(op->S.flags, flags, kFlagBytes, hipMemcpyHostToDevice, op->stream));
+    HIPCHK(hipMemcpyAsync(op->S.norms, &one, sizeof(double), hipMemcpyHostToDevice, op->stream));
+    HIPCHK(hipMemcpyAsync(op->S.alphas, alphas, n * sizeof(double), hipMemcpyHostToDevice,
+                          op->stream));
+    if (n > 1)
+      HIPCHK(hipMemcpyAsync(op->S.betas, betas, (n - 1) * sizeof(double), hipMemcpyHostToDevice,
+                            op->stream));
+    enqueue_ftk_dev(op, n, which == 1 ? kDevExp : kDevInv);
+    HIPCHK(hipMemcpyAsync(y_out, op->S.y, n * sizeof(double), hipMemcpyDeviceToHost, op->stream));
+    HIPCHK(hipMemcpyAsync(flags, op->S.flags, kFlagBytes, hipMemcpyDeviceToHost, op->stream));
+    sync_checked(op);
+    *on_device = flags[4] ? 0 : 1;
   });
 }
 

@@ -126,6 +126,8 @@ tpl_locality_order = _sig("tpl_locality_order", c_int, c_int64, POINTER(c_int64)
                           POINTER(c_int32), c_int32, c_int32, POINTER(c_int32),
                           POINTER(c_int32))
 tpl_op_reorth_second_passes = _sig("tpl_op_reorth_second_passes", c_int, c_void_p, POINTER(c_int64))
+tpl_op_ftk_device = _sig("tpl_op_ftk_device", c_int, c_void_p, c_int, PD, c_size_t, PD, PD,
+                         POINTER(c_int))
 tpl_op_set_order_groups = _sig("tpl_op_set_order_groups", c_int, c_void_p, c_int32)
 tpl_op_order_groups = _sig("tpl_op_order_groups", c_int32, c_void_p)
 
@@ -164,6 +166,7 @@ EXPORTED = [
     "tpl_op_device_bytes", "tpl_op_reorth_second_passes", "tpl_op_set_reorder",
     "tpl_op_permutation", "tpl_locality_order", "tpl_op_tune_order",
     "tpl_last_error_detail", "tpl_op_set_order_groups", "tpl_op_order_groups",
+    "tpl_op_ftk_device",
 ]
 
 

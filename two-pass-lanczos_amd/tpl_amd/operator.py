@@ -216,6 +216,19 @@ class HipCsrOp:
         device, the whole solve one graph, 2 auto (default: device for k <= 128)."""
         check(_lib.tpl_op_set_device_ftk(self._op, int(mode)))
 
+    def ftk_device(self, which: str, alphas, betas):
+        """The device f(T_k) kernel alone ("inv" / "exp") on this operator's GPU:
+        -> (y' = f(T_k) e_1, evaluated on the device?)."""
+        a = np.ascontiguousarray(alphas, dtype=np.float64)
+        b = np.ascontiguousarray(betas, dtype=np.float64)
+        y = np.zeros(a.shape[0])
+        on = ctypes.c_int()
+        check(_lib.tpl_op_ftk_device(self._op, {"inv": 0, "exp": 1}[which],
+                                     a.ctypes.data_as(POINTER(c_double)), a.shape[0],
+                                     b.ctypes.data_as(POINTER(c_double)),
+                                     y.ctypes.data_as(POINTER(c_double)), byref(on)))
+        return y, bool(on.value)
+
     def enable_timing(self, on: bool = True):
         """Record HIP events inside the captured passes of later solves."""
         check(_lib.tpl_op_enable_timing(self._op, 1 if on else 0))
