@@ -384,7 +384,7 @@ void oracle_spmv(const ocsr* A, const osched* S, const double* x, double* y) { s
 /* Building blocks of the partitioned orders (tests/partition_oracle.py composes them):
  * alpha partial total v . w of one operator's rows (device order, or sequential without
  * a schedule), sum of squares (no sqrt), partials() of an array, and the replicated long
- * rows' alpha partials (k_long_epi_p1: blocks of 1024 long rows, thread t accumulates
+ * rows' alpha partials (k_long_epi_p1: blocks of 256 long rows, thread t accumulates
  * fma(v, w) over rows t + 256 q, tree256). */
 double oracle_dot(const osched* S, int64_t n, const double* v, const double* w) {
   if (!S) return dot_faithful(n, v, w);
@@ -401,7 +401,7 @@ double oracle_sumsq(const osched* S, int64_t n, const double* x) {
   return r;
 }
 double oracle_reduce(const double* P, int G) { return reduce_partials(P, G); }
-#define LONG_EPI_ROWS 1024 /* kLongEpiRows (tpl_device.h) */
+#define LONG_EPI_ROWS 256 /* kLongEpiRows (tpl_device.h): one row per thread */
 void oracle_long_alpha_blocks(int64_t nl, const double* v, const double* w, double* out) {
   const int64_t nb = (nl + LONG_EPI_ROWS - 1) / LONG_EPI_ROWS;
   for (int64_t b = 0; b < nb; ++b) {

@@ -20,7 +20,7 @@ between — the element-wise steps are the same IEEE operations on every rank):
   all long rows]; its local CSR (local indices) restricts each long row to the columns
   it owns; a long row = 0 + P_0 + P_1 + ... (rank order) of the ranks' restricted sums;
   alpha = partials([T_0 .. T_{R-1}, LB_0 .. LB_{nb-1}]) (short-row chunk totals, then the
-  long rows' fma blocks of 1024, k_long_epi_p1); the norm of rank r covers its local
+  long rows' fma blocks of 256 (one row per thread), k_long_epi_p1); the norm of rank r covers its local
   elements [0, norm_n) (rank 0: all, others: short rows only: replicated rows once).
 """
 from __future__ import annotations

@@ -140,7 +140,13 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   const double p = block_sum_tail(acc, red);
   // write-through: every k_p1_axpy workgroup, on every XCD, reads all the partials
   // next (measured: pass one -0.2 to -0.3 us per step against a plain store)
-  if (threadIdx.x == 0) st_out(S.Pa + slot, p);
+  if (threadIdx.x == 0)
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(S.Pa + slot),
+                       (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  // replicated partition: the last chunk workgroup forms this rank's alpha total (it
+  // travels with the long-row partials in the same all-gather)
+  if (A.fold_cnt) fold_partials(S.Pa, A.n_chunks, A.fold_cnt, A.fold_pa, red);
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
@@ -217,6 +223,15 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   for (int64_t i0 = i00 + (int64_t)kAxPairs * 2 * kTPB; i0 < end; i0 += 2 * kTPB) // E > 2048
     step(i0, *reinterpret_cast<const double2*>(W + i0),
          *reinterpret_cast<const double2*>(r_cur + i0));
+  if (A.fold_cnt) {  // replicated partition: the last row block forms this rank's norm total
+    const double p = block_sum(acc, red);
+    if (threadIdx.x == 0)
+      __hip_atomic_store(reinterpret_cast<unsigned long long*>(S.Pb + rb),
+                         (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    fold_partials(S.Pb, A.G2, A.fold_cnt + kCntStride, A.fold_pb, red);
+    return;
+  }
   const double p = block_sum_tail(acc, red);
   if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
 }
@@ -624,19 +639,20 @@ __global__ __launch_bounds__(kTPB) void k_permute(int64_t n, int cols, double* _
 // yall[r * n_long + l]; every rank then runs the row's epilogue (identical bits on all
 // ranks). Local index of long row l: A.n - A.n_long + l. Alpha partial (pass one):
 // thread t accumulates fma(v, w) over rows t + 256q of its workgroup's range, tree256.
+// One row per thread (kLongEpiRows = kTPB): the row's R partials and its own vector
+// entries all in flight at once, one round trip (1,024 rows per workgroup took four
+// dependent ones: 4.7 us per launch at 5M arcs, r02). yall: R segments of A.y_ld.
 template <class Epi>
 __device__ __forceinline__ double long_epi_rows(const CsrDev& A, const double* __restrict__ yall,
                                                 int R, const Epi& epi) {
   double acc = 0.0;
-  const int l0 = blockIdx.x * kLongEpiRows;
-  const int l1 = l0 + kLongEpiRows < A.n_long ? l0 + kLongEpiRows : A.n_long;
+  const int l = blockIdx.x * kLongEpiRows + threadIdx.x;
+  if (l >= A.n_long) return acc;
   const int base = (int)(A.n - A.n_long);
-  for (int l = l0 + threadIdx.x; l < l1; l += kTPB) {
-    const auto pre = epi.pre(base + l);
-    double y = 0.0;
-    for (int r = 0; r < R; ++r) y = y + yall[(size_t)r * A.n_long + l];
-    epi.apply(base + l, y, pre, acc);
-  }
+  const auto pre = epi.pre(base + l);
+  double y = 0.0;
+  for (int r = 0; r < R; ++r) y = y + yall[(size_t)r * A.y_ld + l];
+  epi.apply(base + l, y, pre, acc);
   return acc;
 }
 
@@ -660,9 +676,13 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
   epi.W = W;
   epi.Vcol = Vcol;
   epi.Pa_long = nullptr;
+  // the R alpha totals of the short rows (each rank's fold, all-gathered with the long-row
+  // partials) to the contiguous slots k_p1_axpy reduces: Pa_long[-R .. -1]
+  if (blockIdx.x == 0 && (int)threadIdx.x < R)
+    Pa_long[(int)threadIdx.x - R] = yall[(size_t)threadIdx.x * A.y_ld + A.n_long];
   const double acc = long_epi_rows(A, yall, R, epi);
   const double p = block_sum_tail(acc, red);
-  if (threadIdx.x == 0) Pa_long[blockIdx.x] = p;
+  if (threadIdx.x == 0 && blockIdx.x * kLongEpiRows < A.n_long) Pa_long[blockIdx.x] = p;
 }
 
 __global__ __launch_bounds__(kTPB) void k_long_epi_y(CsrDev A, const double* __restrict__ yall,
@@ -959,8 +979,9 @@ int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kL
 hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
                        const double* r_cur, const double* r_prev, double* W, double* Vcol,
                        double* Pa_long, int j, hipStream_t s) {
-  if (A.n_long > 0)
-    hipLaunchKernelGGL(k_long_epi_p1, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A, S, yall, R,
+  // at least one workgroup: it also moves the ranks' short-row alpha totals
+  const int blocks = long_epi_blocks(A) > 0 ? long_epi_blocks(A) : 1;
+  hipLaunchKernelGGL(k_long_epi_p1, dim3(blocks), dim3(kTPB), 0, s, A, S, yall, R,
                        r_cur, r_prev, W, Vcol, Pa_long, j);
   return hipGetLastError();
 }

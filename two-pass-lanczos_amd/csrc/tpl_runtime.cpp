@@ -153,7 +153,9 @@ struct tpl_op_s {
   int64_t ns_local = 0;
   std::vector<int32_t> g2l;
   std::vector<int64_t> local_rows;
-  double* d_yall = nullptr;         // nranks x n_long long-row partials (all-gathered)
+  double* d_yall = nullptr;         // nranks x (n_long + 1): long-row partials + the rank's
+                                    // short-row alpha total (all-gathered together)
+  unsigned int* d_fold = nullptr;   // arrival counters of the rank-total folds (hybrid)
   std::vector<int32_t> h_rowptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
@@ -257,8 +259,11 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.NA_r = op->dist ? op->dist->nranks + (op->hybrid ? long_epi_blocks(op) : 0) : A.NA;
   A.G2_r = op->dist ? op->dist->nranks : A.G2;
   A.long_defer = op->hybrid ? 1 : 0;
-  A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * L.lrows.size() : nullptr;
-  A.pad2 = 0;
+  A.y_ld = (int32_t)L.lrows.size() + 1;
+  A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * A.y_ld : nullptr;
+  A.fold_cnt = op->hybrid ? op->d_fold : nullptr;
+  A.fold_pa = op->hybrid ? A.ypart + L.lrows.size() : nullptr;
+  A.fold_pb = op->hybrid ? op->d_rsum + A.NA_r + op->dist->rank : nullptr;
   A.norm_n = op->hybrid && op->dist->rank != 0 ? op->ns_local : op->n;
   A.s_win = L.s_win;
   A.s_win_max = L.s_win_max;
@@ -555,22 +560,17 @@ void enqueue_p1_prologue(tpl_op_s* op) {
 // the AXPY (the beta total; with row blocks r_{j+1} travels with it).
 void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
   if (op->hybrid) {
-    // short-row alpha total and the long rows' partials travel together; every rank then
-    // finishes the long rows itself (replicated) and adds their alpha once
-    const size_t nl = op->lay.lrows.size();
-    dist_total(op, op->S.Pa, A.n_chunks, op->d_rsum + op->dist->rank);
-    dist_group(op, true);
-    dist_allgather(op, op->d_rsum, 1);
-    if (nl) dist_allgather(op, op->d_yall, nl);
-    dist_group(op, false);
+    // ONE all-gather: each rank's long-row partials and its short-row alpha total (folded
+    // by k_p1_spmv's last chunk workgroup) travel in one segment; every rank then finishes
+    // the long rows itself (replicated) and adds their alpha once (k_long_epi_p1)
+    dist_allgather(op, op->d_yall, (size_t)A.y_ld);
   } else {
     dist_total(op, op->S.Pa, A.NA, op->d_rsum + op->dist->rank);
     dist_allgather(op, op->d_rsum, 1);
   }
 }
 void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
-  if (op->hybrid) {
-    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+  if (op->hybrid) {  // the rank's norm total: folded by k_p1_axpy's last row block
     dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
   } else {
     const int R = op->dist->nranks;
@@ -585,7 +585,7 @@ void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
 void enqueue_p2_exchange(tpl_op_s* op, int j) {
   if (op->hybrid) {
     const size_t nl = op->lay.lrows.size();
-    if (nl) dist_allgather(op, op->d_yall, nl);
+    if (nl) dist_allgather(op, op->d_yall, nl + 1);
   } else {
     dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
   }
@@ -851,9 +851,11 @@ void init_op(tpl_op_s* op) {
     dev_alloc(op, &op->d_rsum, cnt * sizeof(double));
     HIPCHK(hipMemset(op->d_rsum, 0, cnt * sizeof(double)));
     if (op->hybrid) {
-      const size_t ya = std::max<size_t>(nr * op->lay.lrows.size(), 1);
+      const size_t ya = nr * (op->lay.lrows.size() + 1);
       dev_alloc(op, &op->d_yall, ya * sizeof(double));
       HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
+      dev_alloc(op, &op->d_fold, 2 * kCntStride * sizeof(unsigned int));
+      HIPCHK(hipMemset(op->d_fold, 0, 2 * kCntStride * sizeof(unsigned int)));
     }
   }
   HIPCHK(hipEventCreate(&op->ev0));
@@ -1017,7 +1019,7 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
     const CsrDev A = csr_dev(op);
     HIPCHK(launch::spmv(A, op->tmpG, op->W, op->stream));
     if (op->hybrid && A.n_long > 0) {
-      dist_allgather(op, op->d_yall, (size_t)A.n_long);
+      dist_allgather(op, op->d_yall, (size_t)A.y_ld);
       HIPCHK(launch::long_epi_y(A, op->d_yall, op->dist->nranks, op->W, op->stream));
     }
     download_vec(op, y, op->W, 1, mem);
@@ -1338,7 +1340,11 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
     case TPL_KERNEL_EXCHANGE_P2: {
       if (!op->dist) return 0.0;
       const double R = (double)op->dist->nranks;
-      const double vec = op->hybrid ? (double)op->lay.lrows.size() : (double)op->ld;
+      if (op->hybrid) {  // per rank: n_long partials + the alpha total, then the norm total
+        const double nl = (double)op->lay.lrows.size();
+        return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (nl + 2.0) : 8.0 * R * (nl + 1.0);
+      }
+      const double vec = (double)op->ld;
       // pass one: the alpha and beta totals and one vector part per rank; pass two: the
       // vector part only (the row-block pass two gathers v, no totals)
       return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (vec + 2.0) : 8.0 * R * vec;
