@@ -57,6 +57,9 @@ def parse(argv=None):
     p.add_argument("--steps", type=int, default=5)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--k", type=int, default=500)
+    p.add_argument("--f", choices=("inv", "exp"), default="inv",
+                   help="built-in f(T_k) of the timed solve (inv: the headline, configs[2]; "
+                        "exp: configs[1]'s function)")
     p.add_argument("--arcs", type=int, default=0,
                    help="5000/50000/500000 (netgen fixtures) or any other count (synthetic); "
                         "default 500000 at N=1, 5000000 (row-partitioned) at N>1")
@@ -221,9 +224,11 @@ def main():
     torch.cuda.synchronize()
     nloc = int(b_dev.shape[0])
 
+    f_ptr = _lib.FTK_EXP_PTR if args.f == "exp" else _lib.FTK_INV_PTR
+
     def solve():
         check(_lib.tpl_lanczos_two_pass(op.handle, b_dev.data_ptr(), nloc, args.k,
-                                        _lib.FTK_INV_PTR, None, x_dev.data_ptr(),
+                                        f_ptr, None, x_dev.data_ptr(),
                                         _lib.TPL_MEM_DEVICE))
 
     op.enable_timing(True)  # event records inside the captured passes (live timing)
@@ -277,6 +282,12 @@ def main():
             pj = json.load(f)
         traffic, traffic_src = pj["traffic_bytes_per_launch"], pj["source"]
 
+    p1_traffic = None
+    pmc1 = os.path.join(ROOT, "profiles", "pmc_pass_one.json")
+    if os.path.exists(pmc1) and arcs == 500000 and not partitioned and args.k == 500:
+        with open(pmc1) as f:
+            p1_traffic = {k.split("::")[-1]: v["traffic_bytes_per_launch"]
+                          for k, v in json.load(f)["kernels"].items()}
     iters = args.steps * steps_taken
     value = iters / dt
     x_host = x_dev.cpu().numpy()
@@ -341,11 +352,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": data,
-        "config": {"workload": f"lanczos_two_pass k={args.k} f=inv, {arcs}-arc rho=3 KKT "
+        "config": {"workload": f"lanczos_two_pass k={args.k} f={args.f}, {arcs}-arc rho=3 KKT "
                                f"(n={n}, nnz={a.nnz})"
                                + ("" if not partitioned else f", rows partitioned over {world} GPUs"),
                    "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
                    "graphs": op.uses_graphs,
+                   "one_graph_solve": bool(op.flags() & 32),  # f(T_k) on the device
                    # tpl_op_flags bit 6: the device holds the rows in the locality order
                    "row_order": "locality" if op.flags() & 64 else "caller",
                    **({} if partitioned else {"order_groups": op.order_groups()}),
@@ -370,6 +382,7 @@ def main():
                      "frac_fused_bytes": round(b_fused / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
                      "pass1_us_per_step": round(p1_step_us, 3),
                      "frac_pass1_step": round(b_spmv / (p1_step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                     "pass1_traffic_per_launch": p1_traffic,
                      "frac_whole_solve": round((2 * steps_taken - 1) * b_spmv / solve_s / 1e9
                                                / HBM_PEAK_GBS, 4),
                      "kernels_us_isolated": iso},

@@ -22,21 +22,40 @@ with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
 # the headline instance of k_p2_spmv: template variant 122 (500k KKT layout: uniform
 # width 2, int8 values, uint16 chunk and bin columns, chunk window); the other configs of
 # the same bench run (5k, 50k, 5M) instantiate other variants or share it with fewer calls
-HEADLINE = sys.argv[2] if len(sys.argv) > 2 else "k_p2_spmv<122>"
+HEADLINE = sys.argv[2] if len(sys.argv) > 2 else "k_p2_spmv<58>"
 blocks, cur = {}, None
 for l in open(os.path.join(out, "pmc_summary.txt")):
     if not l.startswith(" "):
         cur = l.strip()
         continue
     m = re.match(r"\s+(\S+)\s+([0-9.]+)", l)
-    if m and cur and cur.startswith("k_p2_spmv"):
+    if m and cur:
         blocks.setdefault(cur, {})[m.group(1)] = float(m.group(2))
+SRC = (f"profiles/{tag}_pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE, "
+       "bench.py --headline-only 1 --steps 1 --warmup 0: every launch is the 500k headline's)")
+CFG = "500k-arc KKT, lanczos_two_pass k=500, pinned locality order (bench.py --headline-only 1)"
+
+
+def traffic(vals):
+    return round(2 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024)
+
+
 vals = blocks[HEADLINE]
-d = {"kernel": "k_p2_spmv", "config": "500k-arc KKT, lanczos_two_pass k=500 (bench.py --steps 1 --warmup 0)",
+d = {"kernel": "k_p2_spmv", "config": CFG,
      "FETCH_SIZE_KiB": vals["FETCH_SIZE"], "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
-     "traffic_bytes_per_launch": round(2 * vals["FETCH_SIZE"] * 1024 + vals["WRITE_SIZE"] * 1024),
+     "traffic_bytes_per_launch": traffic(vals),
      "correction": "2 x FETCH_SIZE (gfx950 half-count of wide reads) + WRITE_SIZE",
-     "source": f"profiles/{tag}_pmc_summary.txt (rocprofv3 --pmc FETCH_SIZE, then --pmc WRITE_SIZE)"}
+     "source": SRC}
 with open(os.path.join(prof, "pmc_k_p2_spmv.json"), "w") as f:
     json.dump(d, f, indent=1)
 print(d)
+# pass one at the same size (its counters isolated from the other configs)
+p1 = {"config": CFG, "correction": d["correction"], "source": SRC, "kernels": {}}
+for name, vals in blocks.items():
+    if name.startswith("k_p1_spmv") or name.endswith("k_p1_axpy"):
+        p1["kernels"][name] = {"FETCH_SIZE_KiB": vals["FETCH_SIZE"],
+                               "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
+                               "traffic_bytes_per_launch": traffic(vals)}
+with open(os.path.join(prof, "pmc_pass_one.json"), "w") as f:
+    json.dump(p1, f, indent=1)
+print(p1)

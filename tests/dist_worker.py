@@ -12,6 +12,7 @@ import numpy as np  # noqa: E402
 
 
 def main():
+    os.makedirs(sys.argv[1], exist_ok=True)
     out, transport, arcs, k = sys.argv[1], sys.argv[2], int(sys.argv[3]), int(sys.argv[4])
     mode = sys.argv[5] if len(sys.argv) > 5 else "auto"
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -42,7 +43,7 @@ def main():
              al=dec.alphas, be=dec.betas, steps=dec.steps_taken, bn=dec.b_norm,
              rows=op.local_rows, mode=op.mode, s_short=sch["short_rows"],
              s_long=sch["long_rows"], s_G2=sch["G2"], s_E=sch["E"], s_slices=sch["slices"],
-             starts=getattr(op, "starts", np.zeros(0, dtype=np.int64)))
+             starts=getattr(op, "starts", np.zeros(0, dtype=np.int64)), flags=op.flags())
     torch.cuda.synchronize()
     tdist.barrier()
     op.close()

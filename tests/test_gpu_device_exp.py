@@ -72,6 +72,22 @@ def test_device_exp_random_tridiagonals(op_small, k):
              (rng.standard_normal(k) * 5.0, rng.uniform(0.01, 3.0, k - 1)),
              (rng.uniform(-1000.0, -0.1, k), rng.uniform(0.0, 50.0, k - 1)),   # exp "ill"
              (rng.uniform(-10.0, -0.1, k), rng.uniform(0.0, 1.0, k - 1))]      # exp "well"
+    if k > 200:  # large random T keep e_1 far from the top of the spectrum: add a
+        # Lanczos T_k (diagonal spectrum in [-10, -0.1], random b), the shape the solver sees
+        lam = np.linspace(-10.0, -0.1, 4 * k)
+        v = rng.random(4 * k)
+        v /= np.linalg.norm(v)
+        vp = np.zeros_like(v)
+        al_l, be_l, bprev = [], [], 0.0
+        for _ in range(k):
+            w = lam * v - bprev * vp
+            a_ = v @ w
+            w = w - a_ * v
+            al_l.append(a_)
+            bprev = np.linalg.norm(w)
+            be_l.append(bprev)
+            vp, v = v, w / bprev
+        cases.append((np.array(al_l), np.array(be_l[:k - 1])))
     kept = 0
     for al, be in cases:
         y, on = op_small.ftk_device("exp", al, be)

@@ -30,12 +30,12 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_ranks(tmp, world, transport, mode="auto", arcs=5000, k=50):
+def _run_ranks(tmp, world, transport, mode="auto", arcs=5000, k=50, extra_env=None):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK="0",
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), **(extra_env or {}))
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dist_worker.py"),
                                        tmp, transport, str(arcs), str(k), mode], env=env))
     rcs = [p.wait(timeout=300) for p in procs]
@@ -78,9 +78,12 @@ def _check_exchange_profile(rs):
         assert np.array_equal(r["x3"], r["x1"])
         assert all(t > 0 for t in r["ex_us"])
         b1, b2 = r["ex_bytes"]
-        assert b1 - b2 == 16 * R and b2 > 0
         if str(r["mode"]) == "replicated":
-            assert b2 == 8 * R * len(r["s_long"])
+            # one segment per rank: the n_long partials + the short-row alpha total (pass
+            # one also gathers the norm totals)
+            assert b2 == 8 * R * (len(r["s_long"]) + 1) and b1 - b2 == 8 * R
+        else:
+            assert b1 - b2 == 16 * R and b2 > 0
 
 
 def test_one_rank_rccl_replicated(kkt_tmp, tmp_path):
@@ -91,6 +94,19 @@ def test_one_rank_rccl_replicated(kkt_tmp, tmp_path):
     xr = _assemble([r], "x1", a.shape[0])
     assert np.linalg.norm(xr - x) <= 1e-10 * np.linalg.norm(x)
     _check_partition_order(a, [r], "replicated", 50)
+
+
+@pytest.mark.parametrize("mode", ["replicated", "rows"])
+def test_one_rank_rccl_capture_refused_falls_back_eager(kkt_tmp, tmp_path, mode):
+    """A transport whose exchanges refuse stream capture (forced by the test hook
+    TPL_TEST_REFUSE_CAPTURE): the operator switches to eager launches (run_graph's fallback,
+    tpl_op_flags bit 1) and produces the same bits as the captured graphs."""
+    ref = _run_ranks(str(tmp_path / "g"), 1, "rccl", mode=mode)[0]
+    r = _run_ranks(str(tmp_path / "e"), 1, "rccl", mode=mode,
+                   extra_env={"TPL_TEST_REFUSE_CAPTURE": "1"})[0]
+    assert not int(ref["flags"]) & 2 and int(r["flags"]) & 2
+    for key in ("x1", "x2", "x3", "xs", "al", "be", "y"):
+        assert np.array_equal(r[key], ref[key]), key
 
 
 def _check_partition_order(a, rs, mode, k):

@@ -478,6 +478,12 @@ inline double* rG_of(const tpl_op_s* op, int j) { return j == 1 ? op->bG : op->R
 // In-place all-gather of `count` doubles per rank: rank r's part sits at base + r*count.
 void dist_allgather(tpl_op_s* op, double* base, size_t count) {
   tpl_dist_s* d = op->dist;
+  if (d->comm && std::getenv("TPL_TEST_REFUSE_CAPTURE")) {
+    // test hook: behave like a transport that cannot be captured into a graph
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIPCHK(hipStreamIsCapturing(op->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) fail(TPL_ERR_DEVICE, "exchange refused stream capture (test hook)");
+  }
   if (d->comm) {
     NCCLCHK(ncclAllGather(base + (size_t)d->rank * count, base, count, ncclDouble, d->comm,
                           op->stream));
