@@ -64,11 +64,12 @@ def sq(alphas, betas) -> np.ndarray:
 SOLVERS = {"inv": inv, "exp": exp, "sq": sq}
 
 
-def exp_chebyshev(alphas, betas, rounds: int = 2, shifts: int = 128) -> np.ndarray:
+def exp_chebyshev(alphas, betas, shifts: int = 256) -> np.ndarray:
     """Restatement of the device exp (two-pass-lanczos_amd/csrc/tpl_kernels.hip k_ftk_exp)
     in numpy — TEST INFRASTRUCTURE: it checks the algorithm (Sturm multisection bracket,
     Debye-sized Chebyshev expansion, Clenshaw + Miller's backward Bessel recurrence)
     against LAPACK on the CPU; the device's bits are not reproduced (libm exp/asinh differ).
+    One round of 2 * shifts Sturm shifts over the Gershgorin interval serves both ends.
     Returns y' = exp(T) e_1, or None where the device hands the case back to the host."""
     al = np.asarray(alphas, dtype=np.float64)
     n = len(al)
@@ -95,18 +96,15 @@ def exp_chebyshev(alphas, betas, rounds: int = 2, shifts: int = 128) -> np.ndarr
             c += int(q < 0)
         return c
 
-    brk = [glo, ghi, glo, ghi]
-    for _ in range(rounds):
-        for end in (0, 1):
-            L, U = brk[2 * end], brk[2 * end + 1]
-            need = n if end else 1
-            sig = [L + (U - L) * ((q + 1) / (shifts + 1)) for q in range(shifts)]
-            j = next((q for q in range(shifts) if count(sig[q]) >= need), shifts)
-            brk[2 * end] = L + (U - L) * (j / (shifts + 1)) if j > 0 else L
-            brk[2 * end + 1] = sig[j] if j < shifts else U
+    w = (ghi - glo) / (2 * shifts + 1)
+    cnts = [count(glo + w * (s + 1)) for s in range(2 * shifts)]
+    f0 = next((s for s in range(2 * shifts) if cnts[s] >= 1), 2 * shifts)
+    f1 = next((s for s in range(2 * shifts) if cnts[s] >= n), 2 * shifts)
+    lo_b = glo + w * f0 if f0 > 0 else glo
+    hi_b = glo + w * (f1 + 1) if f1 < 2 * shifts else ghi
     scale = max(abs(glo), abs(ghi))
-    a = brk[0] - 1e-9 * (1.0 + scale)
-    b = brk[3] + 1e-9 * (1.0 + scale)
+    a = lo_b - 1e-9 * (1.0 + scale)
+    b = hi_b + 1e-9 * (1.0 + scale)
     c = 0.5 * (a + b)
     r = max(0.5 * (b - a), 1e-30 * (1.0 + abs(c)))
 

@@ -19,7 +19,19 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 KKT_DIR = os.path.join(GOLDEN, "kkt")
 REF_RESULTS = os.path.join(GOLDEN, "reference_results")
 ELEM_ROWS = 2048   # kElemRows (two-pass-lanczos_amd/csrc/tpl_device.h): rows per element-wise block
+ELEM_MIN_BLOCKS = 192  # kElemMinBlocks
 CHUNK_ROWS = 512   # kChunkRows
+
+
+def elem_layout(n, max_g2=1024):
+    """(G2, E) of the element-wise kernels (tpl_layout.cpp build_layout): kElemRows rows
+    per block, halved down to 512 while that leaves fewer than kElemMinBlocks blocks."""
+    er = ELEM_ROWS
+    while er > 512 and -(-n // er) < ELEM_MIN_BLOCKS:
+        er //= 2
+    g2 = max(1, min(max_g2, -(-n // er)))
+    per = -(-n // g2)
+    return g2, max(512, (per + 511) // 512 * 512)
 
 # md5 of the decompressed netgen .dmx files (regenerated from the reference's own
 # netgen sources + recorded .par seeds; tests/golden/make_fixtures.py)
@@ -156,9 +168,7 @@ def canon_schedule(a, short_row_max=-1, max_g2=1024, reorder=False):
     T = short_row_threshold(lens, short_row_max)
     short = np.nonzero(lens <= T)[0].astype(np.int32)
     long_ = np.nonzero(lens > T)[0].astype(np.int32)
-    g2 = max(1, min(max_g2, -(-n // ELEM_ROWS)))
-    per = -(-n // g2)
-    E = max(512, (per + 511) // 512 * 512)
+    g2, E = elem_layout(n, max_g2)
     return {"short_rows": short, "long_rows": long_, "G2": g2, "E": E,
             "slices": auto_slices(a, long_), "perm": None}
 

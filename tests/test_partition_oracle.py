@@ -13,7 +13,7 @@ import scipy.sparse as sp
 
 import oracle
 from oracle import ftk_ref
-from conftest import canon_schedule, harness_b, short_row_threshold
+from conftest import canon_schedule, elem_layout, harness_b, short_row_threshold
 from partition_oracle import PartitionOracle
 
 K = 40
@@ -27,8 +27,7 @@ def _block_record(a, r0, r1):
     T = short_row_threshold(lens)
     sq = canon_schedule(a)          # slice count: a function of the global column count
     n = r1 - r0
-    g2 = max(1, min(1024, -(-n // 2048)))
-    E = max(512, (-(-n // g2) + 511) // 512 * 512)
+    g2, E = elem_layout(n)
     return {"rows": np.arange(r0, r1), "s_short": np.nonzero(lens <= T)[0].astype(np.int32),
             "s_long": np.nonzero(lens > T)[0].astype(np.int32), "s_G2": g2, "s_E": E,
             "s_slices": sq["slices"]}
@@ -46,8 +45,7 @@ def _replicated_records(a, cuts):
         rows = np.concatenate([S[cuts[r]:cuts[r + 1]], L])
         ns = cuts[r + 1] - cuts[r]
         n = rows.shape[0]
-        g2 = max(1, min(1024, -(-n // 2048)))
-        E = max(512, (-(-n // g2) + 511) // 512 * 512)
+        g2, E = elem_layout(n)
         s = 1
         while s < 8 and n * 8.0 / s > 512 * 1024:
             s *= 2

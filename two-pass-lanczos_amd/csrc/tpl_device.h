@@ -66,6 +66,7 @@ constexpr int kRowsPerThread = kChunkRows / kTPB;
 // re-reduces the ~2.1k alpha partials; fewer workgroups, less of that), 4.94 at 4096
 // (too few workgroups to stream); solve 12.58 vs 12.69 ms.
 constexpr int kElemRows = TPL_ELEM_ROWS;
+constexpr int kElemMinBlocks = 192;  // below this many blocks, kElemRows is halved (to 512)
 constexpr int kShortRowMax = 32;     // upper bound of the short-row threshold
 constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
 constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB table slots)

@@ -21,6 +21,7 @@ namespace tpl {
 // by tpl_debug_stamps().
 constexpr int kMarks = 7;  // marks 0..5 + the workgroup's HW_ID / XCC_ID in slot 6
 __device__ unsigned long long g_stamps[kMarks * 65536];
+__device__ int g_stamps_n;  // k_ftk_exp: the expansion's term count of the last launch
 #define TPL_MARK(k)                                                          \
   do {                                                                       \
     if (threadIdx.x == 0 && blockIdx.x < 65536)                              \

@@ -150,6 +150,10 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
+// NP: alpha partials loaded per thread up front (the launcher picks the smallest of 2, 4,
+// 8, 12 with 256 NP >= NA_r; more are reduced in batches): clamped duplicate loads of a
+// small partial array only cost issue slots and cache traffic.
+template <int NP>
 __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   const double* __restrict__ W,
                                                   const double* __restrict__ r_cur,
@@ -161,7 +165,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k));
   const int rb = elem_block(A, blockIdx.x);
   if (rb < 0) return;
-  PartialRegs<12> pr;
+  PartialRegs<NP> pr;
   const int na_ = A.NA_r;
   load_partials(S.Pa_r, na_, pr);
   const int64_t beg = (int64_t)rb * A.E;
@@ -398,9 +402,10 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
 // product on its own thread, one LDS exchange and barrier per term), the modified Bessel
 // coefficients generated alongside by Miller's backward recurrence I_{m-1} = I_{m+1} +
 // (2m/r) I_m and normalised by e^r = I_0 + 2 sum I_m — no coefficient table, no EVD, and
-// no clusters to resolve (eigenvectors never appear). [a, b]: two rounds of 128-way Sturm
-// multisection per end from the Gershgorin bounds (a count is exact for a matrix within a
-// few ulps of T, so the bracket holds the spectrum up to the added margin). Accuracy is the
+// no clusters to resolve (eigenvectors never appear). [a, b]: one round of 512-shift Sturm
+// multisection of the Gershgorin interval (a count is exact for a matrix within a few ulps
+// of T, so the bracket holds the spectrum up to the added margin; the bracket's excess,
+// at most 1/513 of the Gershgorin width, only scales the error bound by its exponential). Accuracy is the
 // EVD's class: the error is a small multiple of eps * exp(lambda_max) (the coefficients sum
 // to e^b), against the tolerance the host QL itself meets; the terms run until the
 // coefficients fall below 1e-22 of e^b (Debye asymptotics of I_m(r)). Falls back to the host
@@ -411,18 +416,12 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
 constexpr int kExpRows = 8;          // rows per thread: n <= 2048 (the LDS bound is lower)
 constexpr int kExpMaxTerms = 16384;
 constexpr double kExpMinRatio = 1e-3;  // ||exp(T - b I) e_1|| below this: host (see the end)
-__device__ __forceinline__ int sturm_count(const double* al, const double* be, int n,
-                                           double sigma, double pivmin) {
-  double q = al[0] - sigma;
-  if (fabs(q) < pivmin) q = -pivmin;
-  int cnt = q < 0.0;
-  for (int i = 1; i < n; ++i) {
-    const double b = be[i - 1];
-    q = (al[i] - sigma) - (b * b) / q;
-    if (fabs(q) < pivmin) q = -pivmin;
-    cnt += q < 0.0;
-  }
-  return cnt;
+constexpr int kExpShifts = 2 * kTPB;   // Sturm shifts per end of the spectrum (one round)
+// Reciprocal for the Sturm pivots: v_rcp_f64 and one Newton step (a Sturm count tolerates
+// the last-bit difference from a division; the bracket carries a margin far above it)
+__device__ __forceinline__ double rcp_nr(double q) {
+  const double r = __builtin_amdgcn_rcp(q);
+  return fma(fma(-q, r, 1.0), r, r);
 }
 // ln(e^-r I_m(r)), uniform asymptotic (Debye) form; used only to size the expansion
 __device__ __forceinline__ double log_scaled_bessel_i(double m, double r) {
@@ -432,34 +431,44 @@ __device__ __forceinline__ double log_scaled_bessel_i(double m, double r) {
 __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
   extern __shared__ double sh[];
   __shared__ double red[2][kTPB];
-  __shared__ int cnt[kTPB];
-  __shared__ double brk[4];  // [lo_L, lo_U, hi_L, hi_U]
+  __shared__ int cnt[2 * kExpShifts];  // Sturm counts: [min end | max end]
+  __shared__ int first[2];
+  TPL_MARK(0);
   const int n = S.flags[2];
   if (S.flags[1] || n < 1) return;
   const int t = threadIdx.x;
   double* al = sh;            // alpha (n)
-  double* be = sh + n;        // beta (n - 1), be[n-1] = 0
+  double* b2 = sh + n;        // beta^2 (n - 1), b2[n-1] = 0
   double* buf0 = sh + 2 * n;  // Clenshaw exchange buffers: row i at [i + 1], zeros at both ends
   double* buf1 = buf0 + (n + 2);
   const double bnorm = S.norms[0];
-  // load; Gershgorin bounds, largest beta^2, finiteness
+  // this thread's rows: alpha, the betas on both sides (registers for the whole expansion)
+  const int R = (n + kTPB - 1) / kTPB;
+  double ra[kExpRows], rbl[kExpRows], rbr[kExpRows];
   double glo = INFINITY, ghi = -INFINITY, bmax = 0.0;
   bool finite = true;
-  for (int i = t; i < n; i += kTPB) {
-    const double a = S.alphas[i];
-    const double bl = i > 0 ? S.betas[i - 1] : 0.0, br = i + 1 < n ? S.betas[i] : 0.0;
-    al[i] = a;
-    be[i] = br;
-    finite = finite && isfinite(a) && isfinite(br);
-    const double rad = fabs(bl) + fabs(br);
-    glo = fmin(glo, a - rad);
-    ghi = fmax(ghi, a + rad);
-    bmax = fmax(bmax, br * br);
+#pragma unroll
+  for (int u = 0; u < kExpRows; ++u) {
+    const int i = t + u * kTPB;
+    ra[u] = rbl[u] = rbr[u] = 0.0;
+    if (u < R && i < n) {
+      ra[u] = S.alphas[i];
+      rbl[u] = i > 0 ? S.betas[i - 1] : 0.0;
+      rbr[u] = i + 1 < n ? S.betas[i] : 0.0;
+      al[i] = ra[u];
+      b2[i] = rbr[u] * rbr[u];
+      finite = finite && isfinite(ra[u]) && isfinite(rbr[u]);
+      const double rad = fabs(rbl[u]) + fabs(rbr[u]);
+      glo = fmin(glo, ra[u] - rad);
+      ghi = fmax(ghi, ra[u] + rad);
+      bmax = fmax(bmax, rbr[u] * rbr[u]);
+    }
   }
   for (int i = t; i < n + 2; i += kTPB) buf0[i] = buf1[i] = 0.0;
   red[0][t] = glo;
   red[1][t] = ghi;
   cnt[t] = finite ? 0 : 1;
+  if (t < 2) first[t] = kExpShifts;
   __syncthreads();
   for (int h = kTPB / 2; h > 0; h >>= 1) {
     if (t < h) {
@@ -492,64 +501,87 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
     if (t == 0) S.y[0] = exp(al[0]) * bnorm;
     return;
   }
-  // two rounds of 128-way Sturm multisection per end: threads 0..127 bracket lambda_min
-  // (first shift with a count >= 1), threads 128..255 lambda_max (first count == n)
-  if (t == 0) {
-    brk[0] = glo; brk[1] = ghi; brk[2] = glo; brk[3] = ghi;
-  }
-  __syncthreads();
-  constexpr int P = kTPB / 2;
-  const bool hi_end = t >= P;
-  const int tt = hi_end ? t - P : t;
-  for (int round = 0; round < 2; ++round) {
-    const double L = brk[hi_end ? 2 : 0], U = brk[hi_end ? 3 : 1];
-    const double sigma = L + (U - L) * ((double)(tt + 1) / (double)(P + 1));
-    cnt[t] = sturm_count(al, be, n, sigma, pivmin);
+  TPL_MARK(1);
+  // One round of Sturm multisection over the Gershgorin interval [glo, ghi]: 512 shifts
+  // serve both ends, two independent LDL^T pivot chains per thread (ILP: each chain is a
+  // dependent sequence of n reciprocals). lambda_min lies in the bracket ending at the
+  // first shift with a count >= 1, lambda_max in the one ending at the first count == n.
+  {
+    const double w = (ghi - glo) / (double)(kExpShifts + 1);
+    double sg[2], q[2];
+    int c[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      sg[u] = glo + w * (double)(u * kTPB + t + 1);  // shift s = u * 256 + t
+      q[u] = al[0] - sg[u];
+      if (fabs(q[u]) < pivmin) q[u] = -pivmin;
+      c[u] = q[u] < 0.0;
+    }
+    for (int i = 1; i < n; ++i) {
+      const double ai = al[i], bb = b2[i - 1];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        q[u] = (ai - sg[u]) - bb * rcp_nr(q[u]);
+        if (fabs(q[u]) < pivmin) q[u] = -pivmin;
+        c[u] += q[u] < 0.0;
+      }
+    }
+    cnt[t] = c[0];
+    cnt[t + kTPB] = c[1];
     __syncthreads();
-    if (t == 0 || t == P) {
-      const int need = hi_end ? n : 1;
-      int j = 0;
-      while (j < P && cnt[t + j] < need) ++j;
-      const double s_at = [&](int q) { return L + (U - L) * ((double)(q + 1) / (double)(P + 1)); }(j);
-      const double nl = j > 0 ? L + (U - L) * ((double)j / (double)(P + 1)) : L;
-      brk[hi_end ? 2 : 0] = nl;
-      brk[hi_end ? 3 : 1] = j < P ? s_at : U;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int sidx = u * kTPB + t;
+      if (cnt[sidx] >= 1) atomicMin(&first[0], sidx);
+      if (cnt[sidx] >= n) atomicMin(&first[1], sidx);
     }
     __syncthreads();
   }
-  // [a, b] holds the spectrum: the lower end of lambda_min's bracket, the upper end of
-  // lambda_max's, widened by a margin far above a Sturm count's backward error
+  TPL_MARK(2);
+  // [a, b] holds the spectrum: below the shift before lambda_min's first count, above the
+  // first shift counting all n, widened by a margin far above a count's backward error
+  const double wsh = (ghi - glo) / (double)(kExpShifts + 1);
   const double scale = fmax(fabs(glo), fabs(ghi));
-  const double a = brk[0] - 1e-9 * (1.0 + scale);
-  const double b = brk[3] + 1e-9 * (1.0 + scale);
+  const double a = (first[0] > 0 ? glo + wsh * (double)first[0] : glo) - 1e-9 * (1.0 + scale);
+  const double b = (first[1] < kExpShifts ? glo + wsh * (double)(first[1] + 1) : ghi) +
+                   1e-9 * (1.0 + scale);
   const double c = 0.5 * (a + b);
   const double r = fmax(0.5 * (b - a), 1e-30 * (1.0 + fabs(c)));
   const double inv_r = 1.0 / r;
-  // terms: the smallest m with e^-r I_m(r) < 1e-22 (binary search on the asymptotic form),
-  // plus a margin for Miller's start
-  int lo_m = 0, hi_m = kExpMaxTerms;
-  if (log_scaled_bessel_i((double)hi_m, r) >= -50.66) {
+  // terms: the smallest m with e^-r I_m(r) < 1e-22 (asymptotic form, decreasing in m),
+  // found in two parallel passes: every thread tests m = 64 t, then the 64 candidates
+  // below the first passing one
+  {
+    __syncthreads();  // every thread has read the brackets out of first[]
+    if (t < 2) first[t] = kExpMaxTerms + 1;
+    __syncthreads();
+    const int m0 = 64 * t;
+    if (m0 <= kExpMaxTerms && log_scaled_bessel_i((double)m0, r) < -50.66) atomicMin(&first[0], m0);
+    __syncthreads();
+    const int hi = first[0];
+    if (hi <= kExpMaxTerms && t < 64) {
+      const int m1 = hi - 63 + t;
+      if (m1 >= 0 && log_scaled_bessel_i((double)m1, r) < -50.66) atomicMin(&first[1], m1);
+    }
+    __syncthreads();
+  }
+  if (first[0] > kExpMaxTerms) {
     fallback();
     return;
   }
-  while (lo_m < hi_m) {
-    const int mid = (lo_m + hi_m) >> 1;
-    if (log_scaled_bessel_i((double)mid, r) < -50.66) hi_m = mid; else lo_m = mid + 1;
-  }
-  const int N = lo_m + 8;
+  const int N = min(first[0], first[1]) + 8;
+  TPL_MARK(3);
   // Clenshaw: b_m = a_m e_1 + 2 x b_{m+1} - b_{m+2} (m = N .. 1), x = (T - c I) / r; the
   // result is a_0 e_1 + x b_1 - b_2 with a_0 = I_0, a_m = 2 I_m (unnormalised Miller values)
-  const int R = (n + kTPB - 1) / kTPB;
-  double b1[kExpRows], b2[kExpRows];
+  double b1[kExpRows], b2v[kExpRows], dia[kExpRows];
 #pragma unroll
-  for (int u = 0; u < kExpRows; ++u) b1[u] = b2[u] = 0.0;
+  for (int u = 0; u < kExpRows; ++u) {
+    b1[u] = b2v[u] = 0.0;
+    dia[u] = ra[u] - c;
+  }
   double Ip1 = 0.0, Im = 1.0, Ssum = 0.0;  // I_{m+1}, I_m (Miller seed), 2 sum_{m'>=m} I_m'
   double* cur = buf0;
   double* nxt = buf1;
-  auto xprod = [&](const double* v, int i) {  // (x v)_i, v stored at [i + 1]
-    return ((be[i > 0 ? i - 1 : 0] * (i > 0 ? v[i] : 0.0) + (al[i] - c) * v[i + 1]) +
-            be[i] * v[i + 2]) * inv_r;
-  };
   for (int m = N; m >= 1; --m) {
     // publish b_{m+1}, then every row forms b_m from its neighbours
 #pragma unroll
@@ -563,9 +595,10 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
     for (int u = 0; u < kExpRows; ++u) {
       const int i = t + u * kTPB;
       if (u < R && i < n) {
-        double v = 2.0 * xprod(cur, i) - b2[u];
+        const double xb = ((rbl[u] * cur[i] + dia[u] * cur[i + 1]) + rbr[u] * cur[i + 2]) * inv_r;
+        double v = 2.0 * xb - b2v[u];
         if (i == 0) v = v + am;
-        b2[u] = b1[u];
+        b2v[u] = b1[u];
         b1[u] = v;
       }
     }
@@ -576,10 +609,11 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
     if (fabs(Im) > 1e200) {  // Miller's values grow towards m = 0: rescale the whole state
       Im *= 1e-200; Ip1 *= 1e-200; Ssum *= 1e-200;
 #pragma unroll
-      for (int u = 0; u < kExpRows; ++u) { b1[u] *= 1e-200; b2[u] *= 1e-200; }
+      for (int u = 0; u < kExpRows; ++u) { b1[u] *= 1e-200; b2v[u] *= 1e-200; }
     }
     double* sw = cur; cur = nxt; nxt = sw;  // double buffer: one barrier per term
   }
+  TPL_MARK(4);
   // y' = e^b (I_0 e_1 + x b_1 - b_2) / (I_0 + 2 sum I_m)
 #pragma unroll
   for (int u = 0; u < kExpRows; ++u) {
@@ -596,7 +630,8 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
     const int i = t + u * kTPB;
     yv[u] = 0.0;
     if (u < R && i < n) {
-      double v = xprod(cur, i) - b2[u];
+      const double xb = ((rbl[u] * cur[i] + dia[u] * cur[i + 1]) + rbr[u] * cur[i + 2]) * inv_r;
+      double v = xb - b2v[u];
       if (i == 0) v = v + Im;
       yv[u] = v / norm;  // exp(T - b I) e_1
       sq = fma(yv[u], yv[u], sq);
@@ -621,6 +656,10 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
     const int i = t + u * kTPB;
     if (u < R && i < n) S.y[i] = (eb * yv[u]) * bnorm;
   }
+  TPL_MARK(5);
+#if TPL_STAMP
+  if (t == 0) g_stamps_n = N;
+#endif
 }
 
 // Row permutation at the boundary (locality order, tpl_layout.h): out[i] = in[idx[i]] for
@@ -938,7 +977,15 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, hipStream_t s) {
-  hipLaunchKernelGGL(k_p1_axpy, dim3(g2_grid(A)), dim3(kTPB), 0, s, A, S, W, r_cur, r_next, j, k);
+  const dim3 g(g2_grid(A)), b(kTPB);
+  if (A.NA_r <= 2 * kTPB)
+    hipLaunchKernelGGL(k_p1_axpy<2>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+  else if (A.NA_r <= 4 * kTPB)
+    hipLaunchKernelGGL(k_p1_axpy<4>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+  else if (A.NA_r <= 8 * kTPB)
+    hipLaunchKernelGGL(k_p1_axpy<8>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+  else
+    hipLaunchKernelGGL(k_p1_axpy<12>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
   return hipGetLastError();
 }
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
@@ -1032,5 +1079,8 @@ hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip
 #if TPL_STAMP
 extern "C" int tpl_debug_stamps(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps), sizeof(unsigned long long) * tpl::kMarks * n);
+}
+extern "C" int tpl_debug_exp_terms(int* out) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps_n), sizeof(int));
 }
 #endif

@@ -286,7 +286,18 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   }
   if (L.s_col16) std::vector<int32_t>().swap(L.s_col);
   if (L.b_col16) std::vector<int32_t>().swap(L.b_col);
-  const int64_t g2 = (n + kElemRows - 1) / kElemRows;
+  // rows per element-wise workgroup: kElemRows, halved (down to 512) while that leaves
+  // fewer than kElemMinBlocks workgroups — a small operator's element-wise kernels are
+  // pure latency, and more blocks in flight hide it (measured, configs[1] 50k arcs k =
+  // 200: 512 rows 2.50 ms per solve, 1024 2.52, 2048 2.54; the headline 500k: 2048 9.93,
+  // 1024 9.98, 512 10.42 — profiles/r03_small_n_lab.txt)
+  int64_t er = kElemRows;
+  if (sp.elem_rows > 0) {
+    er = ((sp.elem_rows + 511) / 512) * 512;
+  } else {
+    while (er > 512 && (n + er - 1) / er < kElemMinBlocks) er /= 2;
+  }
+  const int64_t g2 = (n + er - 1) / er;
   L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
   const int64_t per = (n + L.G2 - 1) / L.G2;
   L.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);

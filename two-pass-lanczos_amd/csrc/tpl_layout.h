@@ -19,6 +19,8 @@ struct SchedParams {
   int slices = 0;                   // long-row column slices (1, 2, 4, 8); 0 = auto
   bool window = true;               // stage the short chunks' column window in LDS
   int order_groups = 16;            // locality order: long-row rank groups (tpl_layout.h)
+  int elem_rows = 0;                // rows per element-wise workgroup (multiple of 512;
+                                    // 0: kElemRows)
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
