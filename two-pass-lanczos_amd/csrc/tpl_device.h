@@ -142,14 +142,7 @@ struct CsrDev {
   double* ypart;            // n_long partials of this rank (own slice of the all-gather)
   int32_t long_defer;       // 1: long rows deferred to k_long_epi_*
   int32_t y_ld;             // stride of the all-gathered segments: n_long partials + the
-                            // rank's alpha total (yall[r * y_ld + n_long])
-  // Last-arriver folds of the rank totals (replicated partition; nullptr otherwise): the
-  // producers of a partial array (k_p1_spmv's chunk workgroups, k_p1_axpy's row blocks)
-  // count their arrival on fold_cnt[0] / fold_cnt[kCntStride]; the last one reduces the
-  // array in the canonical partials() order into fold_pa / fold_pb.
-  unsigned int* fold_cnt;
-  double* fold_pa;          // this rank's short-row alpha total (yall[rank * y_ld + n_long])
-  double* fold_pb;          // this rank's norm total (DevState::Pb_r[rank])
+                            // rank's short-row alpha total (yall[r * y_ld + n_long])
   int64_t norm_n;           // == n except on ranks that do not own the replicated rows
   // Short-chunk column window (s_win > 0: every chunk's columns lie in [cbase, cbase +
   // s_win), s_win <= kWinMax; the window is staged in LDS). s_win_max: the largest

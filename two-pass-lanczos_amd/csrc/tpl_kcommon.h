@@ -182,42 +182,6 @@ __device__ __forceinline__ double finish_partials_wave(int N, const PartialRegs<
   return (t[0] + t[1]) + (t[2] + t[3]);
 }
 
-// Last-arriver fold of a partial array P[0..N) written by N producer workgroups (one each,
-// stored write-through with st_out): thread 0 drains its stores and adds 1 to *cnt; the
-// workgroup whose add returns N - 1 resets the counter (the next launch starts from 0) and
-// reduces P in the canonical partials() order — reading with agent-scope loads, after its
-// add has returned — into *out. The same hand-off as the long rows' (long_bin), the same
-// bits as a separate reducing kernel (k_reorth_reduce), one kernel boundary fewer. Called
-// by whole workgroups (uniform), after their last use of `red`'s previous contents.
-__device__ __forceinline__ void fold_partials(const double* P, int N, unsigned int* cnt,
-                                              double* out, double* red) {
-  __shared__ int is_last;
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned int arrived =
-        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    is_last = arrived == (unsigned int)(N - 1);
-    if (is_last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!is_last) return;
-  asm volatile("" ::: "memory");
-  const unsigned long long* Pu = reinterpret_cast<const unsigned long long*>(P);
-  double s = 0.0;
-  for (int i0 = threadIdx.x; i0 - (int)threadIdx.x < N; i0 += 8 * kTPB) {
-    unsigned long long t[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      t[u] = __hip_atomic_load(const_cast<unsigned long long*>(Pu) + clampi(i0 + u * kTPB, N - 1),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (i0 + u * kTPB < N) s = s + __longlong_as_double((long long)t[u]);
-  }
-  const double tot = block_sum(s, red);
-  if (threadIdx.x == 0) *out = tot;
-}
-
 // Vector results of a step (w, v_{j+1}, x, r_{j+1}) are consumed only by the NEXT
 // launch. Stored write-through (agent-scope relaxed stores: global_store ... sc1) they
 // leave the XCD's L2 while the kernel runs, instead of as dirty lines written back at

@@ -140,13 +140,7 @@ __global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, 
   const double p = block_sum_tail(acc, red);
   // write-through: every k_p1_axpy workgroup, on every XCD, reads all the partials
   // next (measured: pass one -0.2 to -0.3 us per step against a plain store)
-  if (threadIdx.x == 0)
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(S.Pa + slot),
-                       (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  // replicated partition: the last chunk workgroup forms this rank's alpha total (it
-  // travels with the long-row partials in the same all-gather)
-  if (A.fold_cnt) fold_partials(S.Pa, A.n_chunks, A.fold_cnt, A.fold_pa, red);
+  if (threadIdx.x == 0) st_out(S.Pa + slot, p);
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
@@ -227,15 +221,6 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   for (int64_t i0 = i00 + (int64_t)kAxPairs * 2 * kTPB; i0 < end; i0 += 2 * kTPB) // E > 2048
     step(i0, *reinterpret_cast<const double2*>(W + i0),
          *reinterpret_cast<const double2*>(r_cur + i0));
-  if (A.fold_cnt) {  // replicated partition: the last row block forms this rank's norm total
-    const double p = block_sum(acc, red);
-    if (threadIdx.x == 0)
-      __hip_atomic_store(reinterpret_cast<unsigned long long*>(S.Pb + rb),
-                         (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    fold_partials(S.Pb, A.G2, A.fold_cnt + kCntStride, A.fold_pb, red);
-    return;
-  }
   const double p = block_sum_tail(acc, red);
   if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
 }
@@ -715,7 +700,7 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
   epi.W = W;
   epi.Vcol = Vcol;
   epi.Pa_long = nullptr;
-  // the R alpha totals of the short rows (each rank's fold, all-gathered with the long-row
+  // the R alpha totals of the short rows (each rank's total, all-gathered with the long-row
   // partials) to the contiguous slots k_p1_axpy reduces: Pa_long[-R .. -1]
   if (blockIdx.x == 0 && (int)threadIdx.x < R)
     Pa_long[(int)threadIdx.x - R] = yall[(size_t)threadIdx.x * A.y_ld + A.n_long];

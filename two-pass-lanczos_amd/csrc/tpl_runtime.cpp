@@ -155,7 +155,6 @@ struct tpl_op_s {
   std::vector<int64_t> local_rows;
   double* d_yall = nullptr;         // nranks x (n_long + 1): long-row partials + the rank's
                                     // short-row alpha total (all-gathered together)
-  unsigned int* d_fold = nullptr;   // arrival counters of the rank-total folds (hybrid)
   std::vector<int32_t> h_rowptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
@@ -261,9 +260,6 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.long_defer = op->hybrid ? 1 : 0;
   A.y_ld = (int32_t)L.lrows.size() + 1;
   A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * A.y_ld : nullptr;
-  A.fold_cnt = op->hybrid ? op->d_fold : nullptr;
-  A.fold_pa = op->hybrid ? A.ypart + L.lrows.size() : nullptr;
-  A.fold_pb = op->hybrid ? op->d_rsum + A.NA_r + op->dist->rank : nullptr;
   A.norm_n = op->hybrid && op->dist->rank != 0 ? op->ns_local : op->n;
   A.s_win = L.s_win;
   A.s_win_max = L.s_win_max;
@@ -567,9 +563,10 @@ void enqueue_p1_prologue(tpl_op_s* op) {
 // the AXPY (the beta total; with row blocks r_{j+1} travels with it).
 void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
   if (op->hybrid) {
-    // ONE all-gather: each rank's long-row partials and its short-row alpha total (folded
-    // by k_p1_spmv's last chunk workgroup) travel in one segment; every rank then finishes
-    // the long rows itself (replicated) and adds their alpha once (k_long_epi_p1)
+    // ONE all-gather: each rank's long-row partials and its short-row alpha total travel
+    // in one segment (one collective's latency per SpMV instead of two); every rank then
+    // finishes the long rows itself (replicated) and adds their alpha once (k_long_epi_p1)
+    dist_total(op, op->S.Pa, A.n_chunks, op->d_yall + (size_t)op->dist->rank * A.y_ld + A.n_long);
     dist_allgather(op, op->d_yall, (size_t)A.y_ld);
   } else {
     dist_total(op, op->S.Pa, A.NA, op->d_rsum + op->dist->rank);
@@ -577,7 +574,8 @@ void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
   }
 }
 void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
-  if (op->hybrid) {  // the rank's norm total: folded by k_p1_axpy's last row block
+  if (op->hybrid) {
+    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
     dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
   } else {
     const int R = op->dist->nranks;
@@ -861,8 +859,6 @@ void init_op(tpl_op_s* op) {
       const size_t ya = nr * (op->lay.lrows.size() + 1);
       dev_alloc(op, &op->d_yall, ya * sizeof(double));
       HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
-      dev_alloc(op, &op->d_fold, 2 * kCntStride * sizeof(unsigned int));
-      HIPCHK(hipMemset(op->d_fold, 0, 2 * kCntStride * sizeof(unsigned int)));
     }
   }
   HIPCHK(hipEventCreate(&op->ev0));
