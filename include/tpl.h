@@ -105,8 +105,8 @@ int64_t tpl_op_nnz(tpl_op_t op);
 /* Bit 0: row-partitioned operator; bit 1: passes launched eagerly (no hipGraph —
  * a host transport, or a transport that refused stream capture); bit 2: values kept
  * as int8, bit 3 / bit 4: short-row / long-row column indices kept as uint16 offsets
- * (see tpl_op_set_value_format), bit 5: the last tpl_lanczos_two_pass ran as one
- * device graph (device f(T_k)), bit 6: rows held in the locality order
+ * (see tpl_op_set_value_format), bit 5: the last tpl_lanczos_two_pass / tpl_lanczos
+ * evaluated f(T_k) on the device (one graph, no host round trip), bit 6: rows held in the locality order
  * (tpl_op_set_reorder, tpl_op_permutation; on a replicated-long-row partition the
  * rank's own short rows are in that order and tpl_op_local_rows, not
  * tpl_op_permutation, reports it). -1 if op is NULL.                               */
@@ -190,7 +190,9 @@ int tpl_ftk_sq(const double* alphas, size_t n_alphas, const double* betas, size_
 
 /* ---- high-level API: src/solvers.rs ------------------------------------- */
 /* solvers::lanczos (src/solvers.rs:46-107): standard pass (V_k kept in HBM),
- * f(T_k) on the host, x = ||b|| V_k y' (device GEMV). x_out has n entries.     */
+ * f(T_k), x = ||b|| V_k y' (device GEMV). x_out has n entries. With a built-in f on a
+ * single-GPU operator f(T_k) runs on the device by the rules of tpl_op_set_device_ftk
+ * (no host round trip); any other f is called on the host.                       */
 tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                        tpl_ftk_fn f, void* f_user, double* x_out, int mem);
 /* solvers::lanczos_two_pass (src/solvers.rs:133-175): pass one (scalars only),

@@ -157,3 +157,40 @@ def test_device_inv_device_pointers(kkt5k):
                                     None, xd.data_ptr(), _lib.TPL_MEM_DEVICE))
     torch.cuda.synchronize()
     assert same_bits(xd.cpu().numpy(), x_host)
+
+
+def test_one_pass_device_f(kkt5k):
+    """solvers::lanczos with a built-in f: f(T_k) on the device between the standard pass
+    and the reconstruction GEMV (no host round trip; tpl_op_flags bit 5). inv is bitwise
+    the host path (the same operations; y' unscaled, the GEMV multiplies by ||b||); exp is
+    within the device exp's tolerance; zero b and early breakdown behave as on the host."""
+    a = kkt5k.a
+    op = HipCsrOp(a)
+    b = std_rng_vector(a.shape[0])
+    for k in (1, 2, 40, 128):
+        xd = solvers.lanczos(op, b, k, ftk.INV)
+        assert op.flags() & ONE_GRAPH
+        op.set_device_ftk(False)
+        xh = solvers.lanczos(op, b, k, ftk.INV)
+        assert not op.flags() & ONE_GRAPH
+        op.set_device_ftk(2)
+        assert same_bits_nan(xd, xh), k
+        xe = solvers.lanczos(op, b, k, ftk.EXP)
+        assert op.flags() & ONE_GRAPH
+        op.set_device_ftk(False)
+        xeh = solvers.lanczos(op, b, k, ftk.EXP)
+        op.set_device_ftk(2)
+        assert np.linalg.norm(xe - xeh) <= 1e-12 * np.linalg.norm(xeh), k
+        # one-pass and two-pass through the same device f (reference results/accuracy_*.csv
+        # relative_solution_deviation ~ 1e-16)
+        xt = solvers.lanczos_two_pass(op, b, k, ftk.EXP)
+        assert np.linalg.norm(xe - xt) <= 1e-13 * np.linalg.norm(xt), k
+    solvers.lanczos(op, b, 129, ftk.INV)  # auto: inv on the host above k = 128
+    assert not op.flags() & ONE_GRAPH
+    with pytest.raises(tpl_amd.LanczosError):
+        solvers.lanczos(op, np.zeros_like(b), 10, ftk.INV)
+    d = sp.diags(np.repeat([1.0, 2.0, 3.0], 50)).tocsr()
+    opd = HipCsrOp(d)
+    xd = solvers.lanczos(opd, np.ones(150), 20, ftk.INV)
+    assert opd.flags() & ONE_GRAPH
+    assert np.linalg.norm(xd - 1.0 / np.repeat([1.0, 2.0, 3.0], 50)) < 1e-12

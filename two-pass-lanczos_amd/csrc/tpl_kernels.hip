@@ -310,7 +310,9 @@ __global__ __launch_bounds__(kTPB) void k_p2_tail(int64_t n, DevState S, double*
 // eliminated rows go to LDS, and the back substitution writes y. One-graph solve only
 // (tpl_runtime.cpp): reads steps_taken and ||b|| from the solver state; dynamic LDS:
 // 6 kcap doubles.
-__global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
+// scale: 1 — y = ||b|| y' (two-pass: y_k, src/solvers.rs:169); 0 — y' itself (one-pass:
+// the reconstruction multiplies by ||b||, src/solvers.rs:96-104); x * 1.0 is exact.
+__global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S, int scale) {
   extern __shared__ double sh[];
   const int n = S.flags[2];
   if (S.flags[1] || n < 1) return;
@@ -326,7 +328,7 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S) {
   }
   __syncthreads();
   if (threadIdx.x != 0) return;
-  const double bnorm = S.norms[0];
+  const double bnorm = scale ? S.norms[0] : 1.0;
   double di = al[0], dui = n > 1 ? be[0] : 0.0, bi = 1.0;
   double nx_dl = n > 1 ? be[0] : 0.0, nx_d = n > 1 ? al[1] : 0.0, nx_du = n > 2 ? be[1] : 0.0;
   for (int i = 0; i + 1 < n; ++i) {
@@ -413,7 +415,7 @@ __device__ __forceinline__ double log_scaled_bessel_i(double m, double r) {
   const double s = sqrt(m * m + r * r);
   return -r + s - m * asinh(m / r) - 0.9189385332046727 - 0.25 * log(s * s);
 }
-__global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
+__global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S, int scale) {
   extern __shared__ double sh[];
   __shared__ double red[2][kTPB];
   __shared__ int cnt[2 * kExpShifts];  // Sturm counts: [min end | max end]
@@ -426,7 +428,7 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
   double* b2 = sh + n;        // beta^2 (n - 1), b2[n-1] = 0
   double* buf0 = sh + 2 * n;  // Clenshaw exchange buffers: row i at [i + 1], zeros at both ends
   double* buf1 = buf0 + (n + 2);
-  const double bnorm = S.norms[0];
+  const double bnorm = scale ? S.norms[0] : 1.0;
   // this thread's rows: alpha, the betas on both sides (registers for the whole expansion)
   const int R = (n + kTPB - 1) / kTPB;
   double ra[kExpRows], rbl[kExpRows], rbr[kExpRows];
@@ -526,10 +528,10 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S) {
   // [a, b] holds the spectrum: below the shift before lambda_min's first count, above the
   // first shift counting all n, widened by a margin far above a count's backward error
   const double wsh = (ghi - glo) / (double)(kExpShifts + 1);
-  const double scale = fmax(fabs(glo), fabs(ghi));
-  const double a = (first[0] > 0 ? glo + wsh * (double)first[0] : glo) - 1e-9 * (1.0 + scale);
+  const double gmag = fmax(fabs(glo), fabs(ghi));
+  const double a = (first[0] > 0 ? glo + wsh * (double)first[0] : glo) - 1e-9 * (1.0 + gmag);
   const double b = (first[1] < kExpShifts ? glo + wsh * (double)(first[1] + 1) : ghi) +
-                   1e-9 * (1.0 + scale);
+                   1e-9 * (1.0 + gmag);
   const double c = 0.5 * (a + b);
   const double r = fmax(0.5 * (b - a), 1e-30 * (1.0 + fabs(c)));
   const double inv_r = 1.0 / r;
@@ -728,9 +730,14 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p2(CsrDev A, DevState S,
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
+// steps < 0: steps_taken from the device state (the device-f path, no host round trip).
 __global__ __launch_bounds__(kTPB) void k_gemv_recon(int64_t n, int steps, DevState S,
                                                      const double* __restrict__ V,
                                                      double* __restrict__ x) {
+  if (steps < 0) {
+    if (S.flags[1] || S.flags[4]) return;  // zero b / f handed back to the host
+    steps = S.flags[2];
+  }
   const double bnorm = S.norms[0];
   for (int64_t i = (int64_t)blockIdx.x * kTPB + threadIdx.x; i < n;
        i += (int64_t)gridDim.x * kTPB) {
@@ -991,12 +998,13 @@ hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], 
   hipLaunchKernelGGL(k_p2_tail, dim3(elem_grid(n)), dim3(kTPB), 0, s, n, S, x, V[0], V[1], V[2]);
   return hipGetLastError();
 }
-hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s) {
-  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)6 * kcap * sizeof(double), s, S);
+hipError_t ftk_inv(const DevState& S, int kcap, int scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)6 * kcap * sizeof(double), s, S, scale);
   return hipGetLastError();
 }
-hipError_t ftk_exp(const DevState& S, int kcap, hipStream_t s) {
-  hipLaunchKernelGGL(k_ftk_exp, dim3(1), dim3(kTPB), (size_t)(4 * kcap + 4) * sizeof(double), s, S);
+hipError_t ftk_exp(const DevState& S, int kcap, int scale, hipStream_t s) {
+  hipLaunchKernelGGL(k_ftk_exp, dim3(1), dim3(kTPB), (size_t)(4 * kcap + 4) * sizeof(double), s, S,
+                     scale);
   return hipGetLastError();
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,

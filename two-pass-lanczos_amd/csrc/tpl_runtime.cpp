@@ -37,8 +37,8 @@ hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const do
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
 hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
                    const int32_t* idx, hipStream_t s);
-hipError_t ftk_inv(const DevState& S, int kcap, hipStream_t s);
-hipError_t ftk_exp(const DevState& S, int kcap, hipStream_t s);
+hipError_t ftk_inv(const DevState& S, int kcap, int scale, hipStream_t s);
+hipError_t ftk_exp(const DevState& S, int kcap, int scale, hipStream_t s);
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
                    double* Vcol, int dyn, hipStream_t s);
 // nflush: x terms the step applies (tpl::p2_flush: every third step and the last)
@@ -651,11 +651,16 @@ void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
 // beta (bitwise the host solver's result); pass two is the k - 1 step launches, those at
 // or past steps_taken doing nothing, with x flushed at multiples of 3 only and the
 // pending terms of the last step added by k_p2_tail (the same sums as the host schedule).
-void enqueue_ftk_dev(tpl_op_s* op, size_t k, int f) {
+// y = f(T_k) e_1 from the device alpha / beta, times ||b|| (scale: the two-pass y_k) or not
+// (the one-pass y').
+void enqueue_ftk_only(tpl_op_s* op, size_t k, int f, int scale) {
   if (f == kDevExp)
-    HIPCHK(launch::ftk_exp(op->S, (int)k, op->stream));
+    HIPCHK(launch::ftk_exp(op->S, (int)k, scale, op->stream));
   else
-    HIPCHK(launch::ftk_inv(op->S, (int)k, op->stream));
+    HIPCHK(launch::ftk_inv(op->S, (int)k, scale, op->stream));
+}
+void enqueue_ftk_dev(tpl_op_s* op, size_t k, int f) {
+  enqueue_ftk_only(op, k, f, 1);
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, nullptr, 1, op->stream));
 }
 void enqueue_pass2_dyn_steps(tpl_op_s* op, size_t k) {
@@ -1256,6 +1261,30 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
     check_k(k);
     // 1. standard pass, V_k in HBM (src/solvers.rs:61)
     run_pass_one(op, b, k, mem, true, false);
+    // the built-in inv / exp on the device, then the reconstruction: no host round trip
+    // (the same rules as tpl_lanczos_two_pass; y' unscaled, the GEMV multiplies by ||b||)
+    const bool is_inv = f == &tpl_ftk_inv, is_exp = f == &tpl_ftk_exp;
+    const size_t kmax = !op->device_ftk ? 0
+                        : is_inv ? (op->device_ftk == 1 ? kDevFtkMaxK : kDevFtkAutoK)
+                        : is_exp ? kDevExpMaxK : 0;
+    op->last_one_graph = false;
+    if ((is_inv || is_exp) && !op->dist && k <= kmax) {
+      enqueue_ftk_only(op, k, is_exp ? kDevExp : kDevInv, 0);
+      HIPCHK(launch::gemv_recon(op->n, -1, op->S, op->d_V, op->x, op->stream));
+      const HostDecomp dd = fetch_decomp(op, k);
+      if (dd.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
+      if (dd.steps == 0) {
+        zero_out(op, x_out, mem);
+        return;
+      }
+      if (!dd.flags[4]) {
+        op->last_one_graph = true;
+        download_vec(op, x_out, op->x, 1, mem);
+        sync_checked(op);
+        return;
+      }
+      // handed back to the host (exp only): the host solver below, on the same V_k
+    }
     const HostDecomp d = fetch_decomp(op, k);
     if (d.flags[1]) fail_input("Input vector `b` must not be a zero vector.");
     if (d.steps == 0) { // :64-66
@@ -1401,7 +1430,7 @@ tpl_status tpl_op_ftk_device(tpl_op_t op, int which, const double* alphas, size_
     if (n > 1)
       HIPCHK(hipMemcpyAsync(op->S.betas, betas, (n - 1) * sizeof(double), hipMemcpyHostToDevice,
                             op->stream));
-    enqueue_ftk_dev(op, n, which == 1 ? kDevExp : kDevInv);
+    enqueue_ftk_only(op, n, which == 1 ? kDevExp : kDevInv, 1);
     HIPCHK(hipMemcpyAsync(y_out, op->S.y, n * sizeof(double), hipMemcpyDeviceToHost, op->stream));
     HIPCHK(hipMemcpyAsync(flags, op->S.flags, kFlagBytes, hipMemcpyDeviceToHost, op->stream));
     sync_checked(op);
