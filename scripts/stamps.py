@@ -8,7 +8,7 @@ import numpy as np
 import tpl_amd
 from tpl_amd import _lib
 from tpl_amd.utils.data_loader import load_kkt_system, write_qfc_3line
-K = 6
+K = 7  # kMarks (tpl_kcommon.h): marks 0..5 + the HW_ID / XCC_ID slot
 write_qfc_3line("/tmp/t.qfc", 500000)
 a = load_kkt_system(os.path.join(ROOT, "tests/golden/kkt/netgen-500000-3.dmx.xz"), "/tmp/t.qfc").a
 n = a.shape[0]
