@@ -160,6 +160,7 @@ struct DevState {
   double* alphas;   // alphas[j-1] = alpha_j                              (kcap)
   double* betas;    // betas[j-1]  = beta_j                               (kcap)
   double* y;        // pass-two coefficients y_k (already * ||b||), or y' (kcap)
+  double* p2c;      // pass-two step records, 8 doubles per step (k_p2_coefs, EpiPass2R)
   double* Pa;       // alpha partials (NA) — written by this rank's kernels
   double* Pb;       // ||.||^2 partials (G2)
   // What the reducing kernels read: Pa / Pb on one GPU; with the rows partitioned

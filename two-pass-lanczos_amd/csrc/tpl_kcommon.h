@@ -337,6 +337,61 @@ __device__ __forceinline__ void p2_epi_init(EpiPass2& epi, const DevState& S, co
   p2_epi_coefs(epi, S, j, nflush);
 }
 
+// pass two with the step's coefficients in a record (DevState::p2c, written by k_p2_coefs
+// before the steps): record j = {beta_{j-1} (0 at j = 1), alpha_j, 1/beta_j, y_j, y_{j-1},
+// y_{j-2}, active, 0}. Lane l loads field l & 7 together with its row's own vector entries,
+// i.e. after the gathers, and the epilogue reads the fields with readlane. The unit gather
+// scale is known at entry, so the products, the LDS piece sums and the long rows' hand-off
+// never wait for the coefficients (with scalar coefficient loads, every workgroup waited
+// for a miss to the fabric before its first product: MI355X L2s drop lines other XCDs wrote
+// at each kernel start). Bitwise the same operations as EpiPass2 (1/beta_j is the same IEEE
+// division, made once per step by k_p2_coefs). active = 0: a one-graph solve's launch at or
+// past steps_taken — the SpMV still runs (the arrival counters stay balanced), the
+// epilogue stores nothing.
+struct Pre2R {
+  double vc, vp, x, cv;
+};
+struct EpiPass2R {
+  const double* v_cur;
+  const double* v_prev; // == v_cur (never used) at j == 1 where v_0 = 0
+  const double* rec;    // this step's coefficient record (8 doubles)
+  bool has_prev;
+  int nflush;           // 0..3 x terms applied by this step
+  double* v_next;
+  double* x;
+  double* Vcol;
+  __device__ __forceinline__ Pre2R pre(int i) const {
+    return Pre2R{v_cur[i], v_prev[i], nflush ? x[i] : 0.0, rec[threadIdx.x & 7]};
+  }
+  __device__ __forceinline__ double apply(int i, double s, const Pre2R& p, double&) const {
+    if (readlane_f64(p.cv, 6) == 0.0) return 0.0;  // inactive launch (uniform)
+    const double beta_sub = readlane_f64(p.cv, 0), alpha = readlane_f64(p.cv, 1);
+    const double invb = readlane_f64(p.cv, 2), ycoef = readlane_f64(p.cv, 3);
+    const double vp = has_prev ? p.vp : 0.0;
+    double w = s - beta_sub * vp;
+    w = w - alpha * p.vc;
+    const double vn = w * invb;
+#if TPL_WT_V
+    st_out(v_next + i, vn);
+#else
+    st_plain(v_next + i, vn);
+#endif
+    if (nflush) {
+      double xv = p.x;
+      if (nflush >= 3) xv = xv + readlane_f64(p.cv, 5) * p.vp;
+      if (nflush >= 2) xv = xv + readlane_f64(p.cv, 4) * p.vc;
+#if TPL_WT_X
+      st_out(x + i, xv + ycoef * vn);
+#else
+      st_plain(x + i, xv + ycoef * vn);
+#endif
+    }
+    if (Vcol) Vcol[i] = vn;
+    return vn;
+  }
+  __device__ __forceinline__ void long_alpha(int, double) const {}
+};
+
 // Kernel-argument fields both paths of an SpMV-shaped kernel read, pinned in SGPRs at
 // entry: all kernel-argument loads then share ONE scalar round trip, instead of a second
 // one behind the first branch (hipcc sinks a load into the branch that uses it).
@@ -351,6 +406,7 @@ __device__ __forceinline__ void pin_layout_args(const CsrDev& A) {
 __device__ __forceinline__ void keep_pre(PreNone&) {}
 __device__ __forceinline__ void keep_pre(Pre1& p) { keep(p.rc); keep(p.rp); }
 __device__ __forceinline__ void keep_pre(Pre2& p) { keep(p.vc); keep(p.vp); keep(p.x); }
+__device__ __forceinline__ void keep_pre(Pre2R& p) { keep(p.vc); keep(p.vp); keep(p.x); keep(p.cv); }
 
 // Result of a workgroup's prologue: the gather scale, or "stop" (uniform across the grid).
 struct Scale {

@@ -73,8 +73,17 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1), this rank's rows;
 // xsrc = the gather source holding r_j for every column (== r_cur on one GPU, the
 // all-gathered vector when the rows are partitioned over ranks).
+// Occupancy of k_p1_spmv: its beta chain keeps values live across the whole SpMV (90 VGPRs
+// unconstrained: 5 waves per SIMD, so a 1,536-workgroup grid — 6 per CU at 500k arcs —
+// left 256 chunk workgroups waiting for a slot, chunk start median 2.1 us against 0.3 in
+// k_p2_spmv; scripts/stamps.py). The layouts with int8 values and narrow chunks (the KKT
+// ones) fit 6 waves per SIMD with no spill; the others would spill, so they keep the
+// default bound.
+constexpr int p1_min_waves(int F) {
+  return ((F & 8) && ((F & 7) == 1 || (F & 7) == 2)) ? 6 : TPL_SPMV_MIN_WAVES;
+}
 template <int F>
-__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p1_spmv(CsrDev A, DevState S,
+__global__ __launch_bounds__(kTPB, p1_min_waves(F)) void k_p1_spmv(CsrDev A, DevState S,
                                                   const double* __restrict__ xsrc,
                                                   const double* __restrict__ r_cur,
                                                   const double* __restrict__ r_prev,
@@ -245,35 +254,56 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
   }
 }
 
-// Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x.
+// Pass two, step j = 1 .. steps-1: regenerate v_{j+1}, accumulate x. rec: step j's
+// coefficient record (EpiPass2R: loaded after the gathers, never waited on before the
+// epilogue; the gather scale is 1).
 template <int F>
-__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A, DevState S,
+__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A,
+                                                  const double* __restrict__ rec,
                                                   const double* __restrict__ xsrc,
                                                   const double* __restrict__ v_cur,
                                                   const double* __restrict__ v_prev,
                                                   double* __restrict__ v_next,
                                                   double* __restrict__ x,
                                                   double* __restrict__ Vcol, int j,
-                                                  int nflush, int dyn) {
+                                                  int nflush) {
   extern __shared__ double lds[];
   pin_layout_args(A);
-  asm volatile("" ::"s"(S.betas), "s"(S.alphas), "s"(S.y), "s"(xsrc), "s"(v_cur), "s"(v_prev),
-               "s"(v_next), "s"(x), "s"(Vcol), "s"(j), "s"(nflush), "s"(dyn), "s"(S.flags));
-  EpiPass2 epi;
-  p2_epi_ptrs(epi, v_cur, v_prev, v_next, x, Vcol, j, nflush);
-  // The coefficients are read once the workgroup's entry and vector loads are in
-  // flight (scale_of runs after them): a scalar load waited on at entry would put a
-  // second dependent round trip in front of every workgroup.
-  // dyn (one-graph solve): the graph holds k - 1 step launches; those at or past
-  // steps_taken (pass one broke down early) do nothing.
-  auto coefs = [&]() -> Scale {
-    __builtin_amdgcn_sched_barrier(0);
-    if (dyn && j >= S.flags[2]) return Scale{0.0, false};
-    p2_epi_coefs(epi, S, j, nflush);
-    return Scale{1.0, true};
-  };
+  asm volatile("" ::"s"(rec), "s"(xsrc), "s"(v_cur), "s"(v_prev), "s"(v_next), "s"(x), "s"(Vcol),
+               "s"(j), "s"(nflush));
+  EpiPass2R epi;
+  epi.v_cur = v_cur;
+  epi.v_prev = (j >= 2) ? v_prev : v_cur;
+  epi.rec = rec;
+  epi.has_prev = j >= 2;
+  epi.nflush = nflush;
+  epi.v_next = v_next;
+  epi.x = x;
+  epi.Vcol = Vcol;
   double acc = 0.0;
-  spmv_block<F>(A, xsrc, coefs, epi, acc, lds);
+  spmv_block<F>(A, xsrc, UnitScale{}, epi, acc, lds);
+}
+
+// Pass-two step records (EpiPass2R): record j (1 <= j < k) = {beta_{j-1} (0 at j = 1),
+// alpha_j, 1 / beta_j, y_j, y_{j-1}, y_{j-2} (0 at j = 1), active, 0}. dyn (one-graph
+// solve): active = j < steps_taken (the device-held count), else 1.
+__global__ __launch_bounds__(kTPB) void k_p2_coefs(DevState S, int k, int dyn) {
+  const int j = blockIdx.x * kTPB + threadIdx.x;
+  if (j < 1 || j >= k) return;
+  double* r = S.p2c + 8 * (size_t)j;
+  double2 r01, r23, r45, r67;
+  r01.x = j >= 2 ? S.betas[j - 2] : 0.0;
+  r01.y = S.alphas[j - 1];
+  r23.x = 1.0 / S.betas[j - 1];
+  r23.y = S.y[j];
+  r45.x = S.y[j - 1];
+  r45.y = j >= 2 ? S.y[j - 2] : 0.0;
+  r67.x = dyn ? ((S.flags[1] == 0 && j < S.flags[2]) ? 1.0 : 0.0) : 1.0;
+  r67.y = 0.0;
+  reinterpret_cast<double2*>(r)[0] = r01;
+  reinterpret_cast<double2*>(r)[1] = r23;
+  reinterpret_cast<double2*>(r)[2] = r45;
+  reinterpret_cast<double2*>(r)[3] = r67;
 }
 
 // One-graph solve, after the k - 1 step launches: the x terms still pending at the last
@@ -1009,10 +1039,15 @@ hipError_t ftk_exp(const DevState& S, int kcap, int scale, hipStream_t s) {
 }
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   int nflush, int dyn, hipStream_t s) {
+                   int nflush, hipStream_t s) {
   if (spmv_grid(A) > 0)
-    return TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S, xsrc, v_cur, v_prev, v_next, x, Vcol, j, nflush,
-                         dyn);
+    return TPL_LAUNCH_CW(k_p2_spmv, A, s, A, S.p2c + 8 * (size_t)j, xsrc, v_cur, v_prev, v_next,
+                         x, Vcol, j, nflush);
+  return hipGetLastError();
+}
+hipError_t p2_coefs(const DevState& S, int k, int dyn, hipStream_t s) {
+  if (k > 1)
+    hipLaunchKernelGGL(k_p2_coefs, dim3((k + kTPB - 1) / kTPB), dim3(kTPB), 0, s, S, k, dyn);
   return hipGetLastError();
 }
 int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kLongEpiRows; }

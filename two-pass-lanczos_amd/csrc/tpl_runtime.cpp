@@ -44,7 +44,9 @@ hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, do
 // nflush: x terms the step applies (tpl::p2_flush: every third step and the last)
 hipError_t p2_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* v_cur,
                    const double* v_prev, double* v_next, double* x, double* Vcol, int j,
-                   int nflush, int dyn, hipStream_t s);
+                   int nflush, hipStream_t s);
+// pass-two step records (EpiPass2R) for steps 1 .. k-1; dyn: activity from the device count
+hipError_t p2_coefs(const DevState& S, int k, int dyn, hipStream_t s);
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,
                       hipStream_t s);
 hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
@@ -375,7 +377,11 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->h_state = nullptr;
     op->d_Pr = nullptr;
     const CsrDev A = csr_dev(op);
-    const size_t doubles = (kc + 1) + 3 * kc + (size_t)std::max(A.NA, 1) + (size_t)A.G2;
+    // [.. | Pb G2 | pad to 64 B | p2c: 8 kc step records]
+    const size_t head = kFlagBytes / sizeof(double) + (kc + 1) + 3 * kc +
+                        (size_t)std::max(A.NA, 1) + (size_t)A.G2;
+    const size_t p2c_off = (head + 7) / 8 * 8;  // in doubles from the base (64-B aligned)
+    const size_t doubles = p2c_off - kFlagBytes / sizeof(double) + 8 * kc;
     const size_t bytes = kFlagBytes + doubles * sizeof(double);
     dev_alloc(op, &op->d_state, bytes);
     HIPCHK(hipMemset(op->d_state, 0, bytes));
@@ -389,6 +395,7 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->S.y = op->S.betas + kc;
     op->S.Pa = op->S.y + kc;
     op->S.Pb = op->S.Pa + std::max(A.NA, 1);
+    op->S.p2c = reinterpret_cast<double*>(base) + p2c_off;
     op->S.Pa_r = op->dist ? op->d_rsum : op->S.Pa;
     op->S.Pb_r = op->dist ? op->d_rsum + A.NA_r : op->S.Pb;
     op->kcap = kc;
@@ -619,8 +626,9 @@ void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth) {
   }
 }
 
-void enqueue_pass2_init(tpl_op_s* op, double* Vout) {
+void enqueue_pass2_init(tpl_op_s* op, size_t steps, double* Vout) {
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, 0, op->stream));
+  HIPCHK(launch::p2_coefs(op->S, (int)steps, 0, op->stream));
   if (op->dist && !op->hybrid) dist_allgather(op, op->V2G[1], (size_t)op->ld);
 }
 void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
@@ -630,7 +638,7 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
     const int nflush = p2_flush(j, (int)steps - 1);
     HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
-                           Vcol, j, nflush, 0, op->stream));
+                           Vcol, j, nflush, op->stream));
     if (op->hybrid) {
       enqueue_p2_exchange(op, j);
       HIPCHK(launch::long_epi_p2(A, op->S, op->d_yall, op->dist->nranks, op->V2[j % 3],
@@ -642,7 +650,7 @@ void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
   }
 }
 void enqueue_pass2(tpl_op_s* op, size_t steps, double* Vout) {
-  enqueue_pass2_init(op, Vout);
+  enqueue_pass2_init(op, steps, Vout);
   enqueue_pass2_steps(op, steps, Vout);
 }
 
@@ -662,13 +670,14 @@ void enqueue_ftk_only(tpl_op_s* op, size_t k, int f, int scale) {
 void enqueue_ftk_dev(tpl_op_s* op, size_t k, int f) {
   enqueue_ftk_only(op, k, f, 1);
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, nullptr, 1, op->stream));
+  HIPCHK(launch::p2_coefs(op->S, (int)k, 1, op->stream));
 }
 void enqueue_pass2_dyn_steps(tpl_op_s* op, size_t k) {
   const CsrDev A = csr_dev(op);
   for (int j = 1; j < (int)k; ++j)
     HIPCHK(launch::p2_spmv(A, op->S, op->V2G[j % 3], op->V2[j % 3],
                            j >= 2 ? op->V2[(j - 1) % 3] : nullptr, op->V2[(j + 1) % 3], op->x,
-                           nullptr, j, j % 3 == 0 ? 3 : 0, 1, op->stream));
+                           nullptr, j, j % 3 == 0 ? 3 : 0, op->stream));
 }
 void enqueue_pass2_tail(tpl_op_s* op) {
   HIPCHK(launch::p2_tail(op->n, op->S, op->x, op->V2, op->stream));
@@ -719,7 +728,7 @@ void run_pass2(tpl_op_s* op, size_t steps) {
     run_graph(op, kGPass2, steps, [&] { enqueue_pass2(op, steps, nullptr); });
     return;
   }
-  enqueue_pass2_init(op, nullptr);
+  enqueue_pass2_init(op, steps, nullptr);
   HIPCHK(hipEventRecord(op->tev[2], op->stream));
   run_graph(op, kGPass2Steps, steps, [&] { enqueue_pass2_steps(op, steps, nullptr); });
   HIPCHK(hipEventRecord(op->tev[3], op->stream));
@@ -1489,7 +1498,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
         case TPL_KERNEL_PASS2_SPMV:
           HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3],
                                  op->V2[(i + 1) % 3], op->V2[i % 3], op->x, nullptr, 2,
-                                 i % 3 == 2 ? 3 : 0, 0, op->stream));
+                                 i % 3 == 2 ? 3 : 0, op->stream));
           break;
         case TPL_KERNEL_EXCHANGE_P1:
           enqueue_p1_exchange_a(op, A);
@@ -1511,6 +1520,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
                           op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[2], op->R[2], op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));
+    HIPCHK(launch::p2_coefs(op->S, (int)op->kcap, 0, op->stream));  // step 2's record
     sync_checked(op);
     auto time_eager = [&] {
       launch_one(0);
