@@ -52,7 +52,7 @@ print(d)
 # pass one at the same size (its counters isolated from the other configs)
 p1 = {"config": CFG, "correction": d["correction"], "source": SRC, "kernels": {}}
 for name, vals in blocks.items():
-    if name.startswith("k_p1_spmv") or name.endswith("k_p1_axpy"):
+    if name.startswith(("k_p1_spmv", "k_p1_axpy")):
         p1["kernels"][name] = {"FETCH_SIZE_KiB": vals["FETCH_SIZE"],
                                "WRITE_SIZE_KiB": vals["WRITE_SIZE"],
                                "traffic_bytes_per_launch": traffic(vals)}
