@@ -270,7 +270,8 @@ def main():
     solve_s = dt / args.steps
     # isolated per-kernel event timings (graph of back-to-back launches), diagnostics only
     names = {_lib.TPL_KERNEL_PASS1_SPMV: "k_p1_spmv", _lib.TPL_KERNEL_PASS1_AXPY: "k_p1_axpy",
-             _lib.TPL_KERNEL_PASS2_SPMV: "k_p2_spmv"}
+             _lib.TPL_KERNEL_PASS2_SPMV: "k_p2_spmv",
+             _lib.TPL_KERNEL_PASS1_STEP: "pass1_step"}
     iso = ({} if args.headline_only else
            {names[kk]: round(op.profile_kernel(kk, args.profile_iters)[0], 3) for kk in names})
     # HBM-side traffic of the same kernel from the committed PMC profile (rocprofv3 --pmc

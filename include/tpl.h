@@ -381,7 +381,8 @@ enum {
   /* partitioned operators only (SURVEY.md §8(e) "comm fraction"): the exchanges one
    * step issues, exactly as the pass graphs issue them (rank totals + all-gathers)  */
   TPL_KERNEL_EXCHANGE_P1 = 4, /* a pass-one step's exchanges                           */
-  TPL_KERNEL_EXCHANGE_P2 = 5  /* a pass-two step's exchange                            */
+  TPL_KERNEL_EXCHANGE_P2 = 5, /* a pass-two step's exchange                            */
+  TPL_KERNEL_PASS1_STEP = 6   /* k_p1_spmv then k_p1_axpy (one pass-one step, fixed j)  */
 };
 /* Time `iters` back-to-back launches of one kernel on the operator's stream with
  * HIP events (a warm-up launch first). Returns the average per launch in

@@ -79,9 +79,12 @@ def _check_exchange_profile(rs):
         assert all(t > 0 for t in r["ex_us"])
         b1, b2 = r["ex_bytes"]
         if str(r["mode"]) == "replicated":
-            # one segment per rank: the n_long partials + the short-row alpha total (pass
-            # one also gathers the norm totals)
-            assert b2 == 8 * R * (len(r["s_long"]) + 1) and b1 - b2 == 8 * R
+            # pass two: one segment of n_long partials + 1 per rank; pass one: the n_long
+            # partials + the rank's short-chunk alpha partials (segments as long as the
+            # most chunks of any rank, 512 short rows each), then the norm totals
+            nl = len(r["s_long"])
+            nch = max(-(-(len(q["rows"]) - nl) // 512) for q in rs)
+            assert b2 == 8 * R * (nl + 1) and b1 == 8 * R * (nl + nch + 1)
         else:
             assert b1 - b2 == 16 * R and b2 > 0
 

@@ -204,6 +204,31 @@ def test_determinism(op5k, kkt5k):
     assert np.array_equal(x1, x2) and np.array_equal(x1, x3)
 
 
+def test_profile_kernel_ids(op5k, kkt5k):
+    """tpl_profile_kernel (bench.py's isolated timings): every single-GPU id times its
+    launches and reports SURVEY §8(d)'s bytes; the pass-one step is both launches; the
+    exchange ids need a partitioned operator; a later solve is unaffected."""
+    from tpl_amd import _lib
+    n, nnz = kkt5k.a.shape[0], kkt5k.a.nnz
+    spmv = 12.0 * nnz + 4.0 * (n + 1) + 16.0 * n
+    want = {_lib.TPL_KERNEL_SPMV: spmv, _lib.TPL_KERNEL_PASS1_SPMV: spmv + 8.0 * n,
+            _lib.TPL_KERNEL_PASS1_AXPY: 24.0 * n, _lib.TPL_KERNEL_PASS1_STEP: spmv + 32.0 * n,
+            _lib.TPL_KERNEL_PASS2_SPMV: spmv + 8.0 * n + 16.0 * n / 3.0}
+    b = std_rng_vector(n)
+    x0 = solvers.lanczos_two_pass(op5k, b, 40, ftk.INV)
+    us = {}
+    for kid, by in want.items():
+        us[kid], got = op5k.profile_kernel(kid, 20)
+        assert us[kid] > 0.0 and got == pytest.approx(by, rel=1e-12), kid
+    assert us[_lib.TPL_KERNEL_PASS1_STEP] > us[_lib.TPL_KERNEL_PASS1_SPMV]
+    for kid in (_lib.TPL_KERNEL_EXCHANGE_P1, _lib.TPL_KERNEL_EXCHANGE_P2):
+        with pytest.raises(tpl_amd.TplError):
+            op5k.profile_kernel(kid, 5)
+    with pytest.raises(tpl_amd.TplError):
+        op5k.profile_kernel(99, 5)
+    assert np.array_equal(solvers.lanczos_two_pass(op5k, b, 40, ftk.INV), x0)
+
+
 def test_config1_vs_reference_order(op5k, kkt5k):
     """Config 1: 5k arcs, two-pass k = 50, f = inv: within 1e-10 of the reference-order
     oracle (row-sequential SpMV, sequential dot/norm, LAPACK solve)."""

@@ -141,8 +141,11 @@ struct CsrDev {
   // norm partials cover elements [0, norm_n) only (replicated entries count once).
   double* ypart;            // n_long partials of this rank (own slice of the all-gather)
   int32_t long_defer;       // 1: long rows deferred to k_long_epi_*
-  int32_t y_ld;             // stride of the all-gathered segments: n_long partials + the
-                            // rank's short-row alpha total (yall[r * y_ld + n_long])
+  int32_t y_ld;             // stride of the all-gathered segments. Pass one: n_long
+                            // partials + the rank's short-chunk alpha partials
+                            // (yall[r * y_ld + n_long + c], nch[r] of them); pass two and
+                            // the plain product: n_long + 1
+  const int32_t* nch;       // chunk (alpha partial) count of every rank (hybrid)
   int64_t norm_n;           // == n except on ranks that do not own the replicated rows
   // Short-chunk column window (s_win > 0: every chunk's columns lie in [cbase, cbase +
   // s_win), s_win <= kWinMax; the window is staged in LDS). s_win_max: the largest

@@ -692,26 +692,45 @@ __global__ __launch_bounds__(kTPB) void k_permute(int64_t n, int cols, double* _
 
 // ---------------------------------------- replicated long rows (partitioned solve)
 // Long row l = sum over ranks, in rank order, of the R partials all-gathered into
-// yall[r * n_long + l]; every rank then runs the row's epilogue (identical bits on all
+// yall[r * y_ld + l]; every rank then runs the row's epilogue (identical bits on all
 // ranks). Local index of long row l: A.n - A.n_long + l. Alpha partial (pass one):
 // thread t accumulates fma(v, w) over rows t + 256q of its workgroup's range, tree256.
-// One row per thread (kLongEpiRows = kTPB): the row's R partials and its own vector
-// entries all in flight at once, one round trip (1,024 rows per workgroup took four
-// dependent ones: 4.7 us per launch at 5M arcs, r02). yall: R segments of A.y_ld.
-template <class Epi>
-__device__ __forceinline__ double long_epi_rows(const CsrDev& A, const double* __restrict__ yall,
-                                                int R, const Epi& epi) {
-  double acc = 0.0;
-  const int l = blockIdx.x * kLongEpiRows + threadIdx.x;
-  if (l >= A.n_long) return acc;
-  const int base = (int)(A.n - A.n_long);
-  const auto pre = epi.pre(base + l);
+// One row per thread (kLongEpiRows = kTPB). Every load of the launch — the row's own
+// vector entries, its R partials (8 in flight at a time, at clamped rows, so every lane
+// loads and the adds keep rank order) — is issued before the DevState scalars are read:
+// one round trip behind the boundary instead of a scalar one first (round 3).
+struct LongSum {
+  double t[8];
+};
+// the first 8 ranks' partials of long row lc (clamped: every lane loads) ...
+__device__ __forceinline__ void long_sum_issue(const CsrDev& A, const double* __restrict__ yall,
+                                               int R, int lc, LongSum& q) {
+#pragma unroll
+  for (int u = 0; u < 8; ++u) q.t[u] = yall[(size_t)clampi(u, R - 1) * A.y_ld + lc];
+}
+// ... summed in rank order; more ranks in batches of 8 loads in flight
+__device__ __forceinline__ double long_sum_finish(const CsrDev& A, const double* __restrict__ yall,
+                                                  int R, int lc, const LongSum& q) {
   double y = 0.0;
-  for (int r = 0; r < R; ++r) y = y + yall[(size_t)r * A.y_ld + l];
-  epi.apply(base + l, y, pre, acc);
-  return acc;
+#pragma unroll
+  for (int u = 0; u < 8; ++u)
+    if (u < R) y = y + q.t[u];
+  for (int r0 = 8; r0 < R; r0 += 8) {
+    double t[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) t[u] = yall[(size_t)clampi(r0 + u, R - 1) * A.y_ld + lc];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (r0 + u < R) y = y + t[u];
+  }
+  return y;
 }
 
+// Pass one after the exchange: the long rows' epilogue (w, alpha partials) and, in R more
+// workgroups, each rank's short-chunk alpha total from its all-gathered chunk partials —
+// finish_partials over yall[r * y_ld + n_long ..], the tree k_reorth_reduce applies, so
+// the totals are bitwise those a separate rank-total launch before the all-gather made
+// (r02/r03; that launch is gone). Pa_long[-R .. -1]: the R totals; Pa_long[b]: block b.
 __global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
                                                       const double* __restrict__ yall, int R,
                                                       const double* __restrict__ r_cur,
@@ -720,33 +739,58 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
                                                       double* __restrict__ Vcol,
                                                       double* __restrict__ Pa_long, int j) {
   __shared__ double red[4];
-  if (S.flags[0]) return;  // stopped / breakdown (uniform)
-  const double beta = S.norms[j - 1];
+  const int nbl = (A.n_long + kLongEpiRows - 1) / kLongEpiRows;
+  if ((int)blockIdx.x >= nbl) {  // rank total (uniform per workgroup)
+    const int r = blockIdx.x - nbl;
+    const double* P = yall + (size_t)r * A.y_ld + A.n_long;
+    const int N = A.nch[r];
+    PartialRegs<8> pr;
+    load_partials(P, N, pr);
+    const double tot = finish_partials(P, N, pr, red);
+    if (threadIdx.x == 0) Pa_long[r - R] = tot;
+    return;
+  }
   EpiPass1 epi;
   epi.r_cur = r_cur;
   epi.r_prev = (j >= 2) ? r_prev : r_cur;
   epi.has_prev = j >= 2;
-  epi.invN_cur = 1.0 / beta;
-  epi.invN_prev = (j >= 2) ? 1.0 / S.norms[j - 2] : 0.0;
-  epi.beta_sub = (j >= 2) ? beta : 0.0;
   epi.W = W;
   epi.Vcol = Vcol;
   epi.Pa_long = nullptr;
-  // the R alpha totals of the short rows (each rank's total, all-gathered with the long-row
-  // partials) to the contiguous slots k_p1_axpy reduces: Pa_long[-R .. -1]
-  if (blockIdx.x == 0 && (int)threadIdx.x < R)
-    Pa_long[(int)threadIdx.x - R] = yall[(size_t)threadIdx.x * A.y_ld + A.n_long];
-  const double acc = long_epi_rows(A, yall, R, epi);
+  const int l = blockIdx.x * kLongEpiRows + threadIdx.x;
+  const int lc = l < A.n_long ? l : A.n_long - 1;
+  const int row = (int)(A.n - A.n_long) + lc;
+  const Pre1 pre = epi.pre(row);
+  LongSum q;
+  long_sum_issue(A, yall, R, lc, q);
+  __builtin_amdgcn_sched_barrier(0);
+  const int stop = S.flags[0];
+  const double beta = S.norms[j - 1];
+  const double beta_prev = S.norms[j >= 2 ? j - 2 : 0];
+  const double y = long_sum_finish(A, yall, R, lc, q);
+  if (stop) return;  // stopped / breakdown (uniform)
+  epi.invN_cur = 1.0 / beta;
+  epi.invN_prev = (j >= 2) ? 1.0 / beta_prev : 0.0;
+  epi.beta_sub = (j >= 2) ? beta : 0.0;
+  double acc = 0.0;
+  if (l < A.n_long) epi.apply(row, y, pre, acc);
   const double p = block_sum_tail(acc, red);
-  if (threadIdx.x == 0 && blockIdx.x * kLongEpiRows < A.n_long) Pa_long[blockIdx.x] = p;
+  if (threadIdx.x == 0) Pa_long[blockIdx.x] = p;
 }
 
 __global__ __launch_bounds__(kTPB) void k_long_epi_y(CsrDev A, const double* __restrict__ yall,
                                                      int R, double* __restrict__ y) {
-  long_epi_rows(A, yall, R, EpiSpmv{y});
+  const int l = blockIdx.x * kLongEpiRows + threadIdx.x;
+  const int lc = l < A.n_long ? l : A.n_long - 1;
+  LongSum q;
+  long_sum_issue(A, yall, R, lc, q);
+  const double s = long_sum_finish(A, yall, R, lc, q);
+  if (l < A.n_long) st_out(y + (A.n - A.n_long) + l, s);
 }
 
-__global__ __launch_bounds__(kTPB) void k_long_epi_p2(CsrDev A, DevState S,
+// Pass two after the exchange: the coefficients come from the step's record, loaded
+// lane-wise with the row's own entries (EpiPass2R), so nothing waits for a scalar load.
+__global__ __launch_bounds__(kTPB) void k_long_epi_p2(CsrDev A, const double* __restrict__ rec,
                                                       const double* __restrict__ yall, int R,
                                                       const double* __restrict__ v_cur,
                                                       const double* __restrict__ v_prev,
@@ -754,9 +798,24 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p2(CsrDev A, DevState S,
                                                       double* __restrict__ x,
                                                       double* __restrict__ Vcol, int j,
                                                       int nflush) {
-  EpiPass2 epi;
-  p2_epi_init(epi, S, v_cur, v_prev, v_next, x, Vcol, j, nflush);
-  long_epi_rows(A, yall, R, epi);
+  EpiPass2R epi;
+  epi.v_cur = v_cur;
+  epi.v_prev = (j >= 2) ? v_prev : v_cur;
+  epi.rec = rec;
+  epi.has_prev = j >= 2;
+  epi.nflush = nflush;
+  epi.v_next = v_next;
+  epi.x = x;
+  epi.Vcol = Vcol;
+  const int l = blockIdx.x * kLongEpiRows + threadIdx.x;
+  const int lc = l < A.n_long ? l : A.n_long - 1;
+  const int row = (int)(A.n - A.n_long) + lc;
+  const Pre2R pre = epi.pre(row);
+  LongSum q;
+  long_sum_issue(A, yall, R, lc, q);
+  const double y = long_sum_finish(A, yall, R, lc, q);
+  double acc = 0.0;
+  if (l < A.n_long) epi.apply(row, y, pre, acc);
 }
 
 // One-pass reconstruction x = ||b|| (V_k y') (src/solvers.rs:96-104); V column-major, ld = n.
@@ -1054,10 +1113,9 @@ int long_epi_blocks(const CsrDev& A) { return (A.n_long + kLongEpiRows - 1) / kL
 hipError_t long_epi_p1(const CsrDev& A, const DevState& S, const double* yall, int R,
                        const double* r_cur, const double* r_prev, double* W, double* Vcol,
                        double* Pa_long, int j, hipStream_t s) {
-  // at least one workgroup: it also moves the ranks' short-row alpha totals
-  const int blocks = long_epi_blocks(A) > 0 ? long_epi_blocks(A) : 1;
-  hipLaunchKernelGGL(k_long_epi_p1, dim3(blocks), dim3(kTPB), 0, s, A, S, yall, R,
-                       r_cur, r_prev, W, Vcol, Pa_long, j);
+  // the long rows' blocks, then one workgroup per rank for the short-chunk alpha totals
+  hipLaunchKernelGGL(k_long_epi_p1, dim3(long_epi_blocks(A) + R), dim3(kTPB), 0, s, A, S, yall,
+                     R, r_cur, r_prev, W, Vcol, Pa_long, j);
   return hipGetLastError();
 }
 hipError_t long_epi_y(const CsrDev& A, const double* yall, int R, double* y, hipStream_t s) {
@@ -1069,8 +1127,8 @@ hipError_t long_epi_p2(const CsrDev& A, const DevState& S, const double* yall, i
                        const double* v_cur, const double* v_prev, double* v_next, double* x,
                        double* Vcol, int j, int nflush, hipStream_t s) {
   if (A.n_long > 0)
-    hipLaunchKernelGGL(k_long_epi_p2, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A, S, yall, R,
-                       v_cur, v_prev, v_next, x, Vcol, j, nflush);
+    hipLaunchKernelGGL(k_long_epi_p2, dim3(long_epi_blocks(A)), dim3(kTPB), 0, s, A,
+                       S.p2c + 8 * (size_t)j, yall, R, v_cur, v_prev, v_next, x, Vcol, j, nflush);
   return hipGetLastError();
 }
 hipError_t gemv_recon(int64_t n, int steps, const DevState& S, const double* V, double* x,

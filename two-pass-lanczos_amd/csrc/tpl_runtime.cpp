@@ -155,8 +155,12 @@ struct tpl_op_s {
   int64_t ns_local = 0;
   std::vector<int32_t> g2l;
   std::vector<int64_t> local_rows;
-  double* d_yall = nullptr;         // nranks x (n_long + 1): long-row partials + the rank's
-                                    // short-row alpha total (all-gathered together)
+  double* d_yall = nullptr;         // nranks x y_ld1 (pass one: long-row partials + the
+                                    // rank's short-chunk alpha partials, all-gathered
+                                    // together); pass two: nranks x (n_long + 1)
+  int32_t y_ld1 = 0;                // n_long + the most chunks of any rank
+  std::vector<int32_t> nch;         // chunks (alpha partials) of every rank
+  int32_t* d_nch = nullptr;
   std::vector<int32_t> h_rowptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
@@ -228,7 +232,7 @@ int long_epi_blocks(const tpl_op_s* op) {
   return (int)((op->lay.lrows.size() + kLongEpiRows - 1) / kLongEpiRows);
 }
 
-CsrDev csr_dev(const tpl_op_s* op) {
+CsrDev csr_dev(const tpl_op_s* op, bool pass1 = false) {
   const Layout& L = op->lay;
   CsrDev A;
   A.srows = op->d_srows;
@@ -260,8 +264,9 @@ CsrDev csr_dev(const tpl_op_s* op) {
   A.NA_r = op->dist ? op->dist->nranks + (op->hybrid ? long_epi_blocks(op) : 0) : A.NA;
   A.G2_r = op->dist ? op->dist->nranks : A.G2;
   A.long_defer = op->hybrid ? 1 : 0;
-  A.y_ld = (int32_t)L.lrows.size() + 1;
+  A.y_ld = pass1 && op->hybrid ? op->y_ld1 : (int32_t)L.lrows.size() + 1;
   A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * A.y_ld : nullptr;
+  A.nch = op->d_nch;
   A.norm_n = op->hybrid && op->dist->rank != 0 ? op->ns_local : op->n;
   A.s_win = L.s_win;
   A.s_win_max = L.s_win_max;
@@ -396,6 +401,10 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->S.Pa = op->S.y + kc;
     op->S.Pb = op->S.Pa + std::max(A.NA, 1);
     op->S.p2c = reinterpret_cast<double*>(base) + p2c_off;
+    // hybrid: the chunks' alpha partials go straight into this rank's pass-one segment of
+    // the all-gather (k_long_epi_p1 reduces every rank's after the exchange)
+    if (op->hybrid)
+      op->S.Pa = op->d_yall + (size_t)op->dist->rank * op->y_ld1 + op->lay.lrows.size();
     op->S.Pa_r = op->dist ? op->d_rsum : op->S.Pa;
     op->S.Pb_r = op->dist ? op->d_rsum + A.NA_r : op->S.Pb;
     op->kcap = kc;
@@ -570,11 +579,12 @@ void enqueue_p1_prologue(tpl_op_s* op) {
 // the AXPY (the beta total; with row blocks r_{j+1} travels with it).
 void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
   if (op->hybrid) {
-    // ONE all-gather: each rank's long-row partials and its short-row alpha total travel
-    // in one segment (one collective's latency per SpMV instead of two); every rank then
-    // finishes the long rows itself (replicated) and adds their alpha once (k_long_epi_p1)
-    dist_total(op, op->S.Pa, A.n_chunks, op->d_yall + (size_t)op->dist->rank * A.y_ld + A.n_long);
-    dist_allgather(op, op->d_yall, (size_t)A.y_ld);
+    // ONE all-gather: each rank's long-row partials and its short-chunk alpha partials
+    // travel in one segment (one collective's latency per SpMV); every rank then finishes
+    // the long rows itself (replicated), reduces each rank's alpha partials to its total
+    // and adds the long rows' alpha once (k_long_epi_p1). No rank-total launch sits
+    // between the SpMV and the collective.
+    dist_allgather(op, op->d_yall, (size_t)op->y_ld1);
   } else {
     dist_total(op, op->S.Pa, A.NA, op->d_rsum + op->dist->rank);
     dist_allgather(op, op->d_rsum, 1);
@@ -605,7 +615,7 @@ void enqueue_p2_exchange(tpl_op_s* op, int j) {
 
 // Pass one, step j (k = requested steps).
 void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
-  const CsrDev A = csr_dev(op);
+  const CsrDev A = csr_dev(op, true);
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
                          op->W, Vcol, j, op->stream));
   if (op->dist) enqueue_p1_exchange_a(op, A);
@@ -870,7 +880,15 @@ void init_op(tpl_op_s* op) {
     dev_alloc(op, &op->d_rsum, cnt * sizeof(double));
     HIPCHK(hipMemset(op->d_rsum, 0, cnt * sizeof(double)));
     if (op->hybrid) {
-      const size_t ya = nr * (op->lay.lrows.size() + 1);
+      // every rank's chunk count (each rank's short rows are a contiguous block of the
+      // global split, chunked by kChunkRows: every rank computes all counts alike)
+      if ((int)op->nch.size() != op->dist->nranks ||
+          op->nch[op->dist->rank] != (int32_t)op->lay.c_base.size())
+        fail(TPL_ERR_UNSUPPORTED, "replicated partition: chunk counts disagree with the layout");
+      const int32_t nmax = *std::max_element(op->nch.begin(), op->nch.end());
+      op->y_ld1 = (int32_t)op->lay.lrows.size() + nmax;
+      upload(op, &op->d_nch, op->nch);
+      const size_t ya = nr * (size_t)op->y_ld1;
       dev_alloc(op, &op->d_yall, ya * sizeof(double));
       HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
     }
@@ -1375,15 +1393,18 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
     case TPL_KERNEL_SPMV: return spmv;
     case TPL_KERNEL_PASS1_SPMV: return spmv + 8.0 * n;   // + r_{j-1} read (w is the y write)
     case TPL_KERNEL_PASS1_AXPY: return 24.0 * n;         // w, r_j read; r_{j+1} written
+    case TPL_KERNEL_PASS1_STEP: return spmv + 8.0 * n + 24.0 * n;
     // + v_{j-1} read; x read and written once per three steps (grouped x updates)
     case TPL_KERNEL_PASS2_SPMV: return spmv + 8.0 * n + 16.0 * n / 3.0;
     case TPL_KERNEL_EXCHANGE_P1:
     case TPL_KERNEL_EXCHANGE_P2: {
       if (!op->dist) return 0.0;
       const double R = (double)op->dist->nranks;
-      if (op->hybrid) {  // per rank: n_long partials + the alpha total, then the norm total
+      if (op->hybrid) {  // per rank: n_long partials + its chunk alpha partials (y_ld1),
+        // then the norm total; pass two: n_long partials + 1
         const double nl = (double)op->lay.lrows.size();
-        return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (nl + 2.0) : 8.0 * R * (nl + 1.0);
+        return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (op->y_ld1 + 1.0)
+                                                : 8.0 * R * (nl + 1.0);
       }
       const double vec = (double)op->ld;
       // pass one: the alpha and beta totals and one vector part per rank; pass two: the
@@ -1479,6 +1500,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     set_device(op);
     if (op->kcap < 4) ensure_state(op, 4);
     const CsrDev A = csr_dev(op);
+    const CsrDev A1 = csr_dev(op, true);  // pass-one launches (hybrid: pass-one segment stride)
     const int big = (int)op->kcap; // j < k: the AXPY kernel does its vector work
     // Launch i of the timed sequence. The pass-two kernel rotates its three basis
     // buffers exactly as enqueue_pass2 does (the gathered vector is the previous
@@ -1489,11 +1511,16 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
           HIPCHK(launch::spmv(A, op->V2[0], op->W, op->stream));
           break;
         case TPL_KERNEL_PASS1_SPMV:
-          HIPCHK(launch::p1_spmv(A, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
+          HIPCHK(launch::p1_spmv(A1, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
                                  op->stream));
           break;
         case TPL_KERNEL_PASS1_AXPY:
-          HIPCHK(launch::p1_axpy(A, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
+          HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
+          break;
+        case TPL_KERNEL_PASS1_STEP:  // both pass-one launches, re-running step 2
+          HIPCHK(launch::p1_spmv(A1, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
+                                 op->stream));
+          HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
           HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3],
@@ -1501,8 +1528,8 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
                                  i % 3 == 2 ? 3 : 0, op->stream));
           break;
         case TPL_KERNEL_EXCHANGE_P1:
-          enqueue_p1_exchange_a(op, A);
-          enqueue_p1_exchange_b(op, A, 2);
+          enqueue_p1_exchange_a(op, A1);
+          enqueue_p1_exchange_b(op, A1, 2);
           break;
         case TPL_KERNEL_EXCHANGE_P2:
           enqueue_p2_exchange(op, 2 + i);
@@ -1513,9 +1540,9 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     const bool exchange = kernel == TPL_KERNEL_EXCHANGE_P1 || kernel == TPL_KERNEL_EXCHANGE_P2;
     if (exchange && !op->dist) fail(TPL_ERR_INVALID_ARGUMENT, "exchange ids need a partitioned operator");
     // Valid state for repeated launches: flags clear, partials/norms of a real step.
-    HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
-    HIPCHK(launch::p1_spmv(A, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
-    HIPCHK(launch::p1_axpy(A, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
+    HIPCHK(launch::p1_init(A1, op->S, op->b, op->stream));
+    HIPCHK(launch::p1_spmv(A1, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
+    HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[1], op->b, op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[2], op->R[2], op->n * sizeof(double), hipMemcpyDeviceToDevice,
@@ -1860,6 +1887,9 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
     }
     op->nnz = (int64_t)op->h_col.size();
     op->sp.long_from = ns;
+    op->nch.resize(R);
+    for (int r = 0; r < R; ++r)
+      op->nch[r] = (int32_t)((cut[r + 1] - cut[r] + kChunkRows - 1) / kChunkRows);
     init_op(op.get());
     *out = op.release();
   });

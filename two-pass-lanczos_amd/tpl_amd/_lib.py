@@ -55,6 +55,7 @@ TPL_KERNEL_PASS2_SPMV = 2
 TPL_KERNEL_SPMV = 3
 TPL_KERNEL_EXCHANGE_P1 = 4
 TPL_KERNEL_EXCHANGE_P2 = 5
+TPL_KERNEL_PASS1_STEP = 6
 
 PD = POINTER(c_double)
 
