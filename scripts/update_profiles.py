@@ -15,6 +15,12 @@ prof = os.path.join(ROOT, "profiles")
 shutil.copy(os.path.join(out, "prof", "run_kernel_stats.csv"),
             os.path.join(prof, f"{tag}_kernel_stats.csv"))
 shutil.copy(os.path.join(out, "pmc_summary.txt"), os.path.join(prof, f"{tag}_pmc_summary.txt"))
+# the median per-kernel time from the rocprofv3 kernel trace
+trace = os.path.join(out, "prof", "run_kernel_trace.csv")
+if os.path.exists(trace):
+    import subprocess
+    subprocess.check_call([sys.executable, os.path.join(ROOT, "scripts", "kernel_medians.py"), trace,
+                           os.path.join(prof, f"{tag}_kernel_medians.json")])
 with open(os.path.join(out, "bench.log")) as f:
     line = [l for l in f if l.startswith("{")][-1]
 with open(os.path.join(prof, f"{tag}_bench.json"), "w") as f:
