@@ -2,6 +2,7 @@
 #include "tpl_layout.h"
 
 #include <algorithm>
+#include <unordered_set>
 #include <cmath>
 #include <new>
 #include <string>
@@ -174,14 +175,33 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   L.bin_cap = ((L.bin_cap + kBinMin - 1) / kBinMin) * kBinMin;  // whole load batches
   std::vector<std::vector<std::vector<std::pair<int32_t, int32_t>>>> bins(S); // (r, fill-at-start)
   std::vector<std::vector<int32_t>> fill(S);
+  std::unordered_set<int64_t> lines;  // distinct 128-B lines of the open bin (bin_lines)
+  std::vector<int64_t> plines;
   for (int s = 0; s < S && nlb > 0; ++s) {
+    lines.clear();
     for (size_t r = 0; r < nlb; ++r) {
       const int32_t cnt = poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
+      bool over = false;
+      if (sp.bin_lines > 0) {
+        plines.clear();
+        for (int32_t q = poff[r * (S + 1) + s]; q < poff[r * (S + 1) + s + 1]; ++q)
+          if (!lines.count(cmap(col[q]) >> 4)) plines.push_back(cmap(col[q]) >> 4);
+        std::sort(plines.begin(), plines.end());
+        plines.erase(std::unique(plines.begin(), plines.end()), plines.end());
+        over = !lines.empty() && lines.size() + plines.size() > (size_t)sp.bin_lines;
+      }
       if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
-          (int)bins[s].back().size() == kBinSegs) {
+          (int)bins[s].back().size() == kBinSegs || over) {
         bins[s].emplace_back();
         fill[s].push_back(0);
+        lines.clear();
+        if (sp.bin_lines > 0) {  // recount the piece against the empty bin
+          plines.clear();
+          for (int32_t q = poff[r * (S + 1) + s]; q < poff[r * (S + 1) + s + 1]; ++q)
+            plines.push_back(cmap(col[q]) >> 4);
+        }
       }
+      lines.insert(plines.begin(), plines.end());
       bins[s].back().emplace_back((int32_t)r, fill[s].back());
       fill[s].back() += cnt;
     }

@@ -21,6 +21,8 @@ struct SchedParams {
   int order_groups = 16;            // locality order: long-row rank groups (tpl_layout.h)
   int elem_rows = 0;                // rows per element-wise workgroup (multiple of 512;
                                     // 0: kElemRows)
+  int bin_lines = 0;                // > 0: also close a bin once its gathers would touch
+                                    // more than this many distinct 128-B lines (lab)
 };
 
 // Host copy of the SpMV layout (tpl_device.h).

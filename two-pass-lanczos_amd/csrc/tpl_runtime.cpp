@@ -326,6 +326,7 @@ void rebuild_schedule(tpl_op_s* op) {
   SchedParams sp = op->sp;
   sp.window = !p && !op->local_order;
   if (const char* e = std::getenv("TPL_ELEM_ROWS")) sp.elem_rows = std::atoi(e);  // lab knob
+  if (const char* e = std::getenv("TPL_BIN_LINES")) sp.bin_lines = std::atoi(e);  // lab knob
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
