@@ -68,7 +68,14 @@ constexpr int kRowsPerThread = kChunkRows / kTPB;
 constexpr int kElemRows = TPL_ELEM_ROWS;
 constexpr int kElemMinBlocks = 192;  // below this many blocks, kElemRows is halved (to 512)
 constexpr int kShortRowMax = 32;     // upper bound of the short-row threshold
-constexpr int kSlices = 8;           // column slices of a long row (= XCDs)
+#ifndef TPL_MAX_SLICES
+#define TPL_MAX_SLICES 8
+#endif
+constexpr int kSlices = TPL_MAX_SLICES;  // most column slices of a long row (8 = XCDs)
+#ifndef TPL_SLOT_STRIDE
+#define TPL_SLOT_STRIDE TPL_MAX_SLICES
+#endif
+constexpr int kSlotStride = TPL_SLOT_STRIDE;  // doubles between two long rows' slot arrays
 constexpr int kBinSegs = kTPB - 1;   // pieces per bin (+1 end marker = kTPB table slots)
 // Pieces longer than this are summed by 16 lanes, the others by 8 lanes;
 // the long pieces of a bin come first in its table (CsrDev::b_hdr holds their count).

@@ -721,7 +721,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   // adds of a row are totally ordered at the memory side, so exactly one publisher per
   // launch sees the last count and every slot it reads was drained before the add that
   // preceded its own. No thread ever waits on another: nothing depends on dispatch order.
-  unsigned long long* slots = reinterpret_cast<unsigned long long*>(A.P + (size_t)sg.ri * kSlices);
+  unsigned long long* slots = reinterpret_cast<unsigned long long*>(A.P + (size_t)sg.ri * kSlotStride);
   __hip_atomic_store(slots + s, (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -730,13 +730,43 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("" ::: "memory");  // the slot loads stay behind the returned add
   if ((arrived & (unsigned)(ns - 1)) != (unsigned)(ns - 1)) return;
-  unsigned long long v[kSlices];
+#ifndef TPL_SLOT_LOADS
+#define TPL_SLOT_LOADS TPL_MAX_SLICES
+#endif
+#ifndef TPL_SLOT_WIDE
+#define TPL_SLOT_WIDE (TPL_SLOT_LOADS == 8)  // four 16-B loads (same box, alternated:
+#endif                                     // k_p2_spmv -0.1 us, pass one -0.15 us per step)
+  unsigned long long v[TPL_SLOT_LOADS];
+#if TPL_SLOT_WIDE
+  // 16-B sc1 loads of slot pairs (slot arrays are 64-B aligned). The four loads and their
+  // wait are ONE asm statement: the compiler must not touch the destination registers
+  // between the issue and the s_waitcnt (copying them early reads whatever they held).
+  static_assert(TPL_SLOT_LOADS == 8, "four pairs");
+  typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+  u64x2 r0, r1, r2, r3;
+  const unsigned long long* p0 = slots;
+  const unsigned long long* p1 = slots + (2 < ns ? 2 : 0);
+  const unsigned long long* p2 = slots + (4 < ns ? 4 : 0);
+  const unsigned long long* p3 = slots + (6 < ns ? 6 : 0);
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc1\n\t"
+      "global_load_dwordx4 %1, %5, off sc1\n\t"
+      "global_load_dwordx4 %2, %6, off sc1\n\t"
+      "global_load_dwordx4 %3, %7, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(r0), "=&v"(r1), "=&v"(r2), "=&v"(r3)
+      : "v"(p0), "v"(p1), "v"(p2), "v"(p3)
+      : "memory");
+  v[0] = r0.x; v[1] = r0.y; v[2] = r1.x; v[3] = r1.y;
+  v[4] = r2.x; v[5] = r2.y; v[6] = r3.x; v[7] = r3.y;
+#else
 #pragma unroll
-  for (int k = 0; k < kSlices; ++k)  // slots past the slice count: re-read slot 0
+  for (int k = 0; k < TPL_SLOT_LOADS; ++k)  // slots past the slice count: re-read slot 0
     v[k] = __hip_atomic_load(slots + (k < ns ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
   double y = 0.0;
 #pragma unroll
-  for (int k = 0; k < kSlices; ++k)
+  for (int k = 0; k < TPL_SLOT_LOADS; ++k)
     if (k < ns) y = y + __longlong_as_double((long long)v[k]);
   if (A.long_defer) {  // partitioned: this rank's part of the row; finished after the exchange
     A.ypart[sg.ri] = y;
@@ -788,7 +818,18 @@ __device__ __forceinline__ int spmv_block_impl(const CsrDev& A, const double* __
                                                double* lds) {
   const int b = blockIdx.x;
   if (b < A.n_slice_blocks) {
-    long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, b / A.n_slices, b % A.n_slices, xsrc, scale_of, epi, lds);
+    // bin (m, s) -> block: with S = 8T >= 8 slices, slice s runs on XCD s / T (block
+    // b = 8 (T m + s % T) + s / T), the XCD whose rows its columns are (speed only)
+    int m, s;
+    if (A.n_slices >= 8) {
+      const int T = A.n_slices >> 3, q = b >> 3;
+      s = T * (b & 7) + q % T;
+      m = q / T;
+    } else {
+      m = b / A.n_slices;
+      s = b % A.n_slices;
+    }
+    long_bin<((F >> 3) & 1), ((F >> 5) & 1)>(A, m, s, xsrc, scale_of, epi, lds);
     return -1;
   }
   const int chunk = chunk_of_block(A, b - A.n_slice_blocks);

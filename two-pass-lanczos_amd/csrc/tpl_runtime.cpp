@@ -327,6 +327,8 @@ void rebuild_schedule(tpl_op_s* op) {
   sp.window = !p && !op->local_order;
   if (const char* e = std::getenv("TPL_ELEM_ROWS")) sp.elem_rows = std::atoi(e);  // lab knob
   if (const char* e = std::getenv("TPL_BIN_LINES")) sp.bin_lines = std::atoi(e);  // lab knob
+  if (const char* e = std::getenv("TPL_SLICES"))  // lab knob (auto slice count only)
+    if (sp.slices <= 0) sp.slices = std::atoi(e);
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
@@ -363,7 +365,7 @@ void rebuild_schedule(tpl_op_s* op) {
   upload(op, &op->d_bhdr, L.b_hdr);
   // piece slots, and the arrival counters of the sliced long rows (zero; they run on
   // modulo the slice count across launches)
-  upload(op, &op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlices, 1), 0.0));
+  upload(op, &op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlotStride, 1), 0.0));
   upload(op, &op->d_Pcnt,
          std::vector<unsigned int>(std::max<size_t>(L.lrows.size() * kCntStride, 1), 0u));
   drop_graphs(op);
@@ -1366,8 +1368,9 @@ tpl_status tpl_op_slices(tpl_op_t op, int32_t* slices) {
 tpl_status tpl_op_set_slices(tpl_op_t op, int32_t slices) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
-    if (slices != 0 && slices != 1 && slices != 2 && slices != 4 && slices != 8)
-      fail(TPL_ERR_INVALID_ARGUMENT, "slices must be 0 (auto), 1, 2, 4 or 8");
+    if (slices < 0 || slices > kSlices || (slices & (slices - 1)) != 0)
+      fail(TPL_ERR_INVALID_ARGUMENT,
+           "slices must be 0 (auto) or a power of two up to " + std::to_string(kSlices));
     set_device(op);
     op->sp.slices = slices;
     sync_checked(op);
