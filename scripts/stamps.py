@@ -14,6 +14,7 @@ a = load_kkt_system(os.path.join(ROOT, "tests/golden/kkt/netgen-500000-3.dmx.xz"
 n = a.shape[0]
 b = a @ np.full(n, 1 / np.sqrt(n))
 op = tpl_amd.HipCsrOp(a)
+op.set_order_groups(int(os.environ.get("GROUPS", "13")))  # the benched (pinned) order
 op.set_slices(int(os.environ.get("SLICES", "0")))
 tpl_amd.lanczos_two_pass(op, b, 50, "inv")
 sch = op.schedule()
