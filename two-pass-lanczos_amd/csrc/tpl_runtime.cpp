@@ -325,6 +325,7 @@ void rebuild_schedule(tpl_op_s* op) {
   // 500k): window only in the caller's order.
   SchedParams sp = op->sp;
   sp.window = !p && !op->local_order;
+  if (const char* e = std::getenv("TPL_WINDOW")) sp.window = std::atoi(e) != 0;  // lab knob
   if (const char* e = std::getenv("TPL_ELEM_ROWS")) sp.elem_rows = std::atoi(e);  // lab knob
   if (const char* e = std::getenv("TPL_BIN_LINES")) sp.bin_lines = std::atoi(e);  // lab knob
   if (const char* e = std::getenv("TPL_SLICES"))  // lab knob (auto slice count only)
