@@ -79,8 +79,11 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
 // k_p2_spmv; scripts/stamps.py). The layouts with int8 values and narrow chunks (the KKT
 // ones) fit 6 waves per SIMD with no spill; the others would spill, so they keep the
 // default bound.
+#ifndef TPL_P1_WAVES
+#define TPL_P1_WAVES 6
+#endif
 constexpr int p1_min_waves(int F) {
-  return ((F & 8) && ((F & 7) == 1 || (F & 7) == 2)) ? 6 : TPL_SPMV_MIN_WAVES;
+  return ((F & 8) && ((F & 7) == 1 || (F & 7) == 2)) ? TPL_P1_WAVES : TPL_SPMV_MIN_WAVES;
 }
 template <int F>
 __global__ __launch_bounds__(kTPB, p1_min_waves(F)) void k_p1_spmv(CsrDev A, DevState S,
