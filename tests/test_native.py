@@ -54,3 +54,18 @@ def test_abi_driver_gpu(drivers):
     bitwise equal; one-pass within 1e-10; error statuses; device footprint."""
     dmx, qfc, _ = drivers
     _run([os.path.join(NATIVE, "build", "abi_driver"), dmx, qfc, "--gpu"])
+
+
+def test_cpp_api_cpu(drivers):
+    """include/tpl.hpp: the reference's error Display tests (src/error.rs:70-127) and the
+    StdRng restatement behind its test vectors, no device needed."""
+    _run([os.path.join(NATIVE, "build", "cpp_api_test"), "--cpu"])
+
+
+@pytest.mark.gpu
+def test_cpp_api_gpu(drivers):
+    """The reference's tests through the C++ host API: tests/correctness.rs (inv / exp / z^2,
+    one- and two-pass, diag(1..100), k = 30), src/algorithms/mod.rs's unit tests and its four
+    property tests on the 5k KKT instance (TOLERANCE 5e-9), and the solver-closure errors."""
+    dmx, qfc, _ = drivers
+    _run([os.path.join(NATIVE, "build", "cpp_api_test"), "--gpu", dmx, qfc])
