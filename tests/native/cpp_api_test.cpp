@@ -276,6 +276,37 @@ static void correctness_tests(const tpl::Context& ctx) {
       CHECK(rel < c.tol, "%s %s error too high: %.3e", two ? "Two-pass" : "One-pass", c.name, rel);
     }
   }
+  // LanczosCallback (src/algorithms/mod.rs:82-86): a stop at step 5 returns exactly the
+  // 5-step result; the view carries T_5; an exception in the callback reaches the caller
+  {
+    const auto full = tpl::algorithms::lanczos_standard(a, b, k);
+    size_t seen = 0;
+    bool view_ok = true;
+    const tpl::LanczosCallback stop5 = [&](size_t kk, const double* v, int64_t nn,
+                                           const tpl::TridiagonalSystemView& t) {
+      seen = kk;
+      view_ok = view_ok && v != nullptr && nn == (int64_t)n && t.steps_taken == kk &&
+                t.n_alphas == kk && t.n_betas == kk - 1 && t.alphas[kk - 1] == full.decomposition.alphas[kk - 1];
+      return kk < 5;
+    };
+    const auto cut = tpl::algorithms::lanczos_standard(a, b, k, &stop5);
+    CHECK(seen == 5 && view_ok && cut.decomposition.steps_taken == 5, "callback stop at 5 (seen %zu)", seen);
+    bool same = cut.v_k.cols == 5;
+    for (size_t i = 0; same && i < 5; ++i) same = cut.decomposition.alphas[i] == full.decomposition.alphas[i];
+    for (size_t i = 0; same && i < n * 5; ++i) same = cut.v_k.data[i] == full.v_k.data[i];
+    CHECK(same, "a stopped run is the truncated full run, bit for bit");
+    const tpl::LanczosCallback boom = [](size_t kk, const double*, int64_t, const tpl::TridiagonalSystemView&) -> bool {
+      if (kk == 3) throw std::runtime_error("callback failed");
+      return true;
+    };
+    bool rethrown = false;
+    try {
+      tpl::algorithms::lanczos_standard(a, b, k, &boom);
+    } catch (const std::runtime_error& e) {
+      rethrown = std::string(e.what()) == "callback failed";
+    }
+    CHECK(rethrown, "an exception in the callback reaches the caller");
+  }
   // a C++ closure (not a built-in: called on the host between the passes) gives the same x
   const tpl::FtkSolver user_sq = [](const Vec& al, const Vec& be) {
     const size_t s = al.size();
