@@ -85,6 +85,18 @@ constexpr int kBigPiece = 64;
 #endif
 constexpr int kBinMin = TPL_BIN_MIN; // default entries per bin
 constexpr int kBinBatch = kBinMin / kTPB;  // entries per thread per load batch
+// Device order of the stored entries (speed only; positions, and so every sum, are
+// unchanged): the kBinBatch entries thread t reads from a bin's load batch (positions
+// u0 + 256u + t) are stored consecutively at u0 + kBinBatch t + u, and the
+// kRowsPerThread x W entries of a chunk of uniform width W in {1, 2, 4} (entry k of
+// position C c + 256q + t) at C W c + kRowsPerThread W t + W q + k — one 16-B load of
+// uint16 columns and one 8-B load of int8 values per thread instead of 16 strided
+// 2-B / 1-B loads (tpl_layout.h packed_bin_index / packed_chunk_index).
+#ifndef TPL_PACKED_ENTRIES
+#define TPL_PACKED_ENTRIES 1
+#endif
+constexpr bool kPackedEntries = TPL_PACKED_ENTRIES != 0;
+constexpr bool packed_chunk_width(int w) { return kPackedEntries && (w == 1 || w == 2 || w == 4); }
 constexpr int kLongEpiRows = kTPB;  // one replicated long row per thread (k_long_epi_*)
 constexpr int kWinMax = 2048;        // short-chunk column window in LDS: at most this many columns
 constexpr int kWinLoads = kWinMax / 256;  // window loads per thread

@@ -436,10 +436,55 @@ __device__ __forceinline__ int col_at(const void* p, int i, int base) {
   return reinterpret_cast<const int32_t*>(p)[i];
 }
 
+// A thread's run of N consecutive stored entries (tpl_device.h kPackedEntries), read
+// with the widest loads its bytes allow (16 / 8 / 4 / 2 B per load).
+template <int N, class T>
+__device__ __forceinline__ void load_run(const T* __restrict__ p, T (&out)[N]) {
+  constexpr int B = N * (int)sizeof(T);
+  if constexpr (B >= 16) {
+    static_assert(B % 16 == 0, "whole 16-B loads");
+#pragma unroll
+    for (int i = 0; i < B / 16; ++i) {
+      const uint4 q = reinterpret_cast<const uint4*>(p)[i];
+      __builtin_memcpy(reinterpret_cast<char*>(out) + 16 * i, &q, 16);
+    }
+  } else if constexpr (B == 8) {
+    const uint2 q = *reinterpret_cast<const uint2*>(p);
+    __builtin_memcpy(out, &q, 8);
+  } else if constexpr (B == 4) {
+    const unsigned int q = *reinterpret_cast<const unsigned int*>(p);
+    __builtin_memcpy(out, &q, 4);
+  } else {
+    static_assert(B == 2, "2-B run");
+    const unsigned short q = *reinterpret_cast<const unsigned short*>(p);
+    __builtin_memcpy(out, &q, 2);
+  }
+}
+template <int C16> struct ColType { typedef int32_t T; };
+template <> struct ColType<1> { typedef uint16_t T; };
+template <int V8> struct ValType { typedef double T; };
+template <> struct ValType<1> { typedef int8_t T; };
+// Entries [e0, e0 + N) of a packed run: columns (-1: padding) and values.
+template <int N, int V8, int C16>
+__device__ __forceinline__ void load_entry_run(const void* colp, const void* valp, int e0, int cbase,
+                                               int (&c)[N], double (&a)[N]) {
+  typename ColType<C16>::T cr[N];
+  typename ValType<V8>::T vr[N];
+  load_run<N>(reinterpret_cast<const typename ColType<C16>::T*>(colp) + e0, cr);
+  load_run<N>(reinterpret_cast<const typename ValType<V8>::T*>(valp) + e0, vr);
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    if (C16) c[u] = cr[u] == 0xFFFF ? -1 : cbase + (int)cr[u];
+    else c[u] = (int)cr[u];
+    a[u] = (double)vr[u];
+  }
+}
+
 // ------------------------------------------------------ short rows (sliced ELL)
 // Chunk with a compile-time width W (entries loaded unconditionally: the sliced-ELL
 // storage is allocated for whole chunks, padding has col = -1).
-template <int W, int V8, int C16, int WIN, class Epi, class ScaleFn>
+// PK: the entries are stored in the packed device order (tpl_device.h packed_chunk_width).
+template <int W, int V8, int C16, int WIN, bool PK, class Epi, class ScaleFn>
 __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int base,
                                               const double* __restrict__ xsrc, ScaleFn scale_of,
                                               const Epi& epi, double& acc, double* lds) {
@@ -471,14 +516,28 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
   // the row's own vector entries (needed only by the epilogue), then the gathers.
   int c[kRowsPerThread][W];
   double a[kRowsPerThread][W], xv[kRowsPerThread][W];
+  if constexpr (PK) {  // packed: this thread's kRowsPerThread x W entries are consecutive
+    int cr[kRowsPerThread * W];
+    double ar[kRowsPerThread * W];
+    load_entry_run<kRowsPerThread * W, V8, C16>(A.s_col, A.s_val, base + t * kRowsPerThread * W,
+                                                 cbase, cr, ar);
 #pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q)
+    for (int q = 0; q < kRowsPerThread; ++q)
 #pragma unroll
-    for (int k = 0; k < W; ++k) {
-      const int e = base + k * kChunkRows + q * kTPB + t;
-      c[q][k] = col_at<C16>(A.s_col, e, cbase);
-      a[q][k] = val_at<V8>(A.s_val, e);
-    }
+      for (int k = 0; k < W; ++k) {
+        c[q][k] = cr[q * W + k];
+        a[q][k] = ar[q * W + k];
+      }
+  } else {
+#pragma unroll
+    for (int q = 0; q < kRowsPerThread; ++q)
+#pragma unroll
+      for (int k = 0; k < W; ++k) {
+        const int e = base + k * kChunkRows + q * kTPB + t;
+        c[q][k] = col_at<C16>(A.s_col, e, cbase);
+        a[q][k] = val_at<V8>(A.s_val, e);
+      }
+  }
 #if !TPL_PRE_LATE
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
@@ -573,7 +632,7 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
                                             const double* __restrict__ xsrc, ScaleFn scale_of,
                                             const Epi& epi, double& acc, double* lds) {
   if (CW > 0)
-    return short_chunk_w<CW, V8, C16, (CW > 0 && C16) ? WIN : 0>(
+    return short_chunk_w<CW, V8, C16, (CW > 0 && C16) ? WIN : 0, packed_chunk_width(CW)>(
         A, chunk, chunk * kChunkRows * CW, xsrc, scale_of, epi, acc, lds);
   int W, base;
   if (A.s_width > 0) {
@@ -584,15 +643,32 @@ __device__ __forceinline__ bool short_chunk(const CsrDev& A, int chunk,
     base = A.c_base[chunk];
   }
   switch (W) {
-    case 1: return short_chunk_w<1, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
-    case 2: return short_chunk_w<2, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
-    case 3: return short_chunk_w<3, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
-    case 4: return short_chunk_w<4, V8, C16, 0>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 1: return short_chunk_w<1, V8, C16, 0, false>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 2: return short_chunk_w<2, V8, C16, 0, false>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 3: return short_chunk_w<3, V8, C16, 0, false>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
+    case 4: return short_chunk_w<4, V8, C16, 0, false>(A, chunk, base, xsrc, scale_of, epi, acc, lds);
     default: return short_chunk_any<V8, C16>(A, chunk, base, W, xsrc, scale_of, epi, acc);
   }
 }
 
 // ------------------------------------------------------ long rows (bins)
+// Thread t's entries u = 0 .. kBinBatch-1 of the load batch at e0: positions e0 + 256u + t
+// (stored at e0 + kBinBatch t + u when packed, tpl_device.h kPackedEntries).
+template <int V8, int C16>
+__device__ __forceinline__ void load_bin_batch(const CsrDev& A, int e0, int cbase, int (&c)[kBinBatch],
+                                               double (&a)[kBinBatch]) {
+  const int t = threadIdx.x;
+  if constexpr (kPackedEntries) {
+    load_entry_run<kBinBatch, V8, C16>(A.b_col, A.b_val, e0 + kBinBatch * t, cbase, c, a);
+  } else {
+#pragma unroll
+    for (int u = 0; u < kBinBatch; ++u) {
+      c[u] = col_at<C16>(A.b_col, e0 + u * kTPB + t, cbase);
+      a[u] = val_at<V8>(A.b_val, e0 + u * kTPB + t);
+    }
+  }
+}
+
 // Bin m of slice s. Thread t loads entries t + 256u of the bin (coalesced, at
 // computed addresses) and its bin-table slot; the products go to LDS; each piece is
 // then summed by one wave (lane-strided + butterfly) and handed back to thread j,
@@ -612,11 +688,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   // (its slot index waits on the header).
   int c[kBinBatch];
   double a[kBinBatch], xv[kBinBatch];
-#pragma unroll
-  for (int u = 0; u < kBinBatch; ++u) {
-    c[u] = col_at<C16>(A.b_col, base + u * kTPB + t, cbase);
-    a[u] = val_at<V8>(A.b_val, base + u * kTPB + t);
-  }
+  load_bin_batch<V8, C16>(A, base, cbase, c, a);
   __builtin_amdgcn_sched_barrier(0);
   // only the slots up to the end marker are read (threads past it re-read the marker)
   const int npieces = hdr & 0xFFFF, nbig = hdr >> 16;
@@ -635,11 +707,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = a[u] * (xv[u] * sc.s);
   keep_pre(pre);
   for (int u0 = kBinBatch * kTPB; u0 < A.bin_cap; u0 += kBinBatch * kTPB) { // bins wider than one batch (rare)
-#pragma unroll
-    for (int u = 0; u < kBinBatch; ++u) {
-      c[u] = col_at<C16>(A.b_col, base + u0 + u * kTPB + t, cbase);
-      a[u] = val_at<V8>(A.b_val, base + u0 + u * kTPB + t);
-    }
+    load_bin_batch<V8, C16>(A, base + u0, cbase, c, a);
 #pragma unroll
     for (int u = 0; u < kBinBatch; ++u) xv[u] = xsrc[c[u] < 0 ? 0 : c[u]];
 #pragma unroll

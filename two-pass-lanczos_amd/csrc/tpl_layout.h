@@ -65,6 +65,27 @@ struct ColMap {
   }
 };
 
+// Device order of the entry arrays (tpl_device.h kPackedEntries): the device index of
+// canonical entry i of the bins (bin_cap entries per bin) / of the sliced-ELL chunks of
+// uniform width W (packed_chunk_width(W)).
+inline int64_t packed_bin_index(int64_t i, int32_t bin_cap) {
+  const int64_t bin = i / bin_cap, off = i % bin_cap;
+  const int64_t u0 = off / kBinMin * kBinMin, r = off % kBinMin;
+  return bin * bin_cap + u0 + (r % kTPB) * kBinBatch + r / kTPB;
+}
+inline int64_t packed_chunk_index(int64_t i, int32_t W) {
+  const int64_t per = (int64_t)W * kChunkRows, c = i / per, off = i % per;
+  const int64_t k = off / kChunkRows, p = off % kChunkRows, q = p / kTPB, t = p % kTPB;
+  return c * per + t * (kRowsPerThread * W) + q * W + k;
+}
+// v (canonical order) in the device order idx(i).
+template <class T, class Idx>
+std::vector<T> to_device_order(const std::vector<T>& v, Idx idx) {
+  std::vector<T> out(v.size());
+  for (size_t i = 0; i < v.size(); ++i) out[(size_t)idx((int64_t)i)] = v[i];
+  return out;
+}
+
 // Short-row threshold: requested (> 0), or the auto rule T = clamp(2 * median row nnz,
 // 4, kShortRowMax).
 int32_t short_row_threshold(int64_t n, const std::vector<int32_t>& rp, int requested);

@@ -342,26 +342,30 @@ void rebuild_schedule(tpl_op_s* op) {
   op->vext_cols = 0;
   if (p) dev_alloc(op, &op->d_stage, (size_t)op->n * sizeof(double));
   upload(op, &op->d_srows, L.srows);
+  // entries in the device order (tpl_device.h kPackedEntries; positions unchanged)
+  const bool pack_s = packed_chunk_width(L.s_width);
+  auto sidx = [&](int64_t i) { return pack_s ? packed_chunk_index(i, L.s_width) : i; };
+  auto bidx = [&](int64_t i) { return kPackedEntries ? packed_bin_index(i, L.bin_cap) : i; };
   if (L.s_col16)
-    upload(op, reinterpret_cast<uint16_t**>(&op->d_scol), L.s_col16v);
+    upload(op, reinterpret_cast<uint16_t**>(&op->d_scol), to_device_order(L.s_col16v, sidx));
   else
-    upload(op, reinterpret_cast<int32_t**>(&op->d_scol), L.s_col);
+    upload(op, reinterpret_cast<int32_t**>(&op->d_scol), to_device_order(L.s_col, sidx));
   upload(op, &op->d_scbase, L.s_cbase);
   if (L.val_i8)
-    upload(op, reinterpret_cast<int8_t**>(&op->d_sval), L.s_val8);
+    upload(op, reinterpret_cast<int8_t**>(&op->d_sval), to_device_order(L.s_val8, sidx));
   else
-    upload(op, reinterpret_cast<double**>(&op->d_sval), L.s_val);
+    upload(op, reinterpret_cast<double**>(&op->d_sval), to_device_order(L.s_val, sidx));
   upload(op, &op->d_cbase, L.c_base);
   upload(op, &op->d_cwidth, L.c_width);
   if (L.b_col16)
-    upload(op, reinterpret_cast<uint16_t**>(&op->d_bcol), L.b_col16v);
+    upload(op, reinterpret_cast<uint16_t**>(&op->d_bcol), to_device_order(L.b_col16v, bidx));
   else
-    upload(op, reinterpret_cast<int32_t**>(&op->d_bcol), L.b_col);
+    upload(op, reinterpret_cast<int32_t**>(&op->d_bcol), to_device_order(L.b_col, bidx));
   upload(op, &op->d_bcbase, L.b_cbase);
   if (L.val_i8)
-    upload(op, reinterpret_cast<int8_t**>(&op->d_bval), L.b_val8);
+    upload(op, reinterpret_cast<int8_t**>(&op->d_bval), to_device_order(L.b_val8, bidx));
   else
-    upload(op, reinterpret_cast<double**>(&op->d_bval), L.b_val);
+    upload(op, reinterpret_cast<double**>(&op->d_bval), to_device_order(L.b_val, bidx));
   upload(op, &op->d_bseg, L.b_seg);
   upload(op, &op->d_bhdr, L.b_hdr);
   // piece slots, and the arrival counters of the sliced long rows (zero; they run on
