@@ -10,6 +10,12 @@ import sys
 import numpy as np
 import pytest
 
+# Under pytest-xdist every worker would start one OpenMP thread per core in the oracle
+# library, and the spin-waiting teams oversubscribe the CPUs (measured: the accuracy-CSV
+# test 0.9 s alone, 676 s with -n 4). One thread per worker; set before libgomp loads.
+if os.environ.get("PYTEST_XDIST_WORKER"):
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 for p in (ROOT, os.path.join(ROOT, "two-pass-lanczos_amd")):
     if p not in sys.path:
