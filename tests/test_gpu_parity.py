@@ -589,6 +589,17 @@ def test_int8_value_format_bitwise(kkt_tmp):
     assert np.array_equal(d8.alphas, d64.alphas) and np.array_equal(d8.betas, d64.betas)
     op2 = tpl_amd.HipCsrOp(a * 0.5)
     assert not op2.int8_values
+    # +-2 values: int8 as well; bitwise the oracle on the same layout
+    a2 = (a * 2.0).tocsr()
+    op3 = tpl_amd.HipCsrOp(a2)
+    assert op3.int8_values and int(_lib.tpl_op_flags(op3.handle)) & 24 == 24
+    o3 = canon(op3, a2)
+    d3 = tpl_amd.algorithms.lanczos_pass_one(op3, b, 60)
+    al, be, st, bn, _ = o3.pass_one(b, 60)
+    assert np.array_equal(d3.alphas, al) and np.array_equal(d3.betas, be)
+    x3 = tpl_amd.lanczos_two_pass(op3, b, 60, "inv")  # device inv: bitwise the host's
+    assert np.array_equal(x3, o3.lanczos_two_pass(b, 60, ftk.INV))
+    op3.close()
 
 
 def test_synthetic_generator_instance_bitwise():
