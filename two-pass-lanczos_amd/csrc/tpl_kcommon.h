@@ -212,6 +212,28 @@ __device__ __forceinline__ void st_out(double* p, double v) {
 #endif
 }
 
+// Store flavour of a vector result: 0 plain, 1 write-through (st_out), 2 non-temporal
+// (lab variants only; the shipped flavours are the macros' defaults).
+template <int K>
+__device__ __forceinline__ void st_kind(double* p, double v) {
+  if constexpr (K == 2) __builtin_nontemporal_store(v, p);
+  else if constexpr (K == 1) st_out(p, v);
+  else st_plain(p, v);
+}
+
+// The previous basis vector's own-row load (its last use in the step): plain, or a
+// non-temporal hint (lab variant TPL_NT_PREV=1).
+#ifndef TPL_NT_PREV
+#define TPL_NT_PREV 0
+#endif
+__device__ __forceinline__ double ld_prev(const double* p) {
+#if TPL_NT_PREV
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+
 // Pins a value as computed unconditionally: without it the compiler sinks the loads
 // feeding a product used under a select (padding entries) into a branch, where they
 // issue late behind an s_waitcnt vmcnt(0) and serialise the workgroup's round trips.
@@ -243,7 +265,7 @@ struct EpiPass1 {
   double* W;
   double* Vcol;         // standard variant: column j-1 of V_k, else nullptr
   double* Pa_long;      // alpha partials of the long rows (Pa + n_chunks)
-  __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
+  __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], ld_prev(r_prev + i)}; }
   // long row r: its alpha partial is the single rounded product v * w
   __device__ __forceinline__ void long_alpha(int r, double acc) const { st_out(Pa_long + r, acc); }
   // returns v_j[i]
@@ -251,11 +273,7 @@ struct EpiPass1 {
     const double v = p.rc * invN_cur;
     const double vp = has_prev ? p.rp * invN_prev : 0.0;
     const double w = s - beta_sub * vp;
-#if TPL_WT_W
-    st_out(W + i, w);
-#else
-    st_plain(W + i, w);
-#endif
+    st_kind<TPL_WT_W>(W + i, w);
     if (Vcol) Vcol[i] = v;
     acc = fma(v, w, acc);
     return v;
@@ -281,7 +299,7 @@ struct EpiPass2 {
   double* x;
   double* Vcol; // lanczos_pass_two_with_basis: column j of V'_k, else nullptr
   __device__ __forceinline__ Pre2 pre(int i) const {
-    return Pre2{v_cur[i], v_prev[i], nflush ? x[i] : 0.0};
+    return Pre2{v_cur[i], ld_prev(v_prev + i), nflush ? x[i] : 0.0};
   }
   // returns v_{j+1}[i]
   __device__ __forceinline__ double apply(int i, double s, const Pre2& p, double&) const {
@@ -289,20 +307,12 @@ struct EpiPass2 {
     double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
-#if TPL_WT_V
-    st_out(v_next + i, vn);
-#else
-    st_plain(v_next + i, vn);
-#endif
+    st_kind<TPL_WT_V>(v_next + i, vn);
     if (nflush) {
       double xv = p.x;
       if (nflush >= 3) xv = xv + ycoef2 * p.vp;
       if (nflush >= 2) xv = xv + ycoef1 * p.vc;
-#if TPL_WT_X
-      st_out(x + i, xv + ycoef * vn);
-#else
-      st_plain(x + i, xv + ycoef * vn);
-#endif
+      st_kind<TPL_WT_X>(x + i, xv + ycoef * vn);
     }
     if (Vcol) Vcol[i] = vn;
     return vn;
@@ -361,7 +371,7 @@ struct EpiPass2R {
   double* x;
   double* Vcol;
   __device__ __forceinline__ Pre2R pre(int i) const {
-    return Pre2R{v_cur[i], v_prev[i], nflush ? x[i] : 0.0, rec[threadIdx.x & 7]};
+    return Pre2R{v_cur[i], ld_prev(v_prev + i), nflush ? x[i] : 0.0, rec[threadIdx.x & 7]};
   }
   __device__ __forceinline__ double apply(int i, double s, const Pre2R& p, double&) const {
     if (readlane_f64(p.cv, 6) == 0.0) return 0.0;  // inactive launch (uniform)
@@ -371,20 +381,12 @@ struct EpiPass2R {
     double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
-#if TPL_WT_V
-    st_out(v_next + i, vn);
-#else
-    st_plain(v_next + i, vn);
-#endif
+    st_kind<TPL_WT_V>(v_next + i, vn);
     if (nflush) {
       double xv = p.x;
       if (nflush >= 3) xv = xv + readlane_f64(p.cv, 5) * p.vp;
       if (nflush >= 2) xv = xv + readlane_f64(p.cv, 4) * p.vc;
-#if TPL_WT_X
-      st_out(x + i, xv + ycoef * vn);
-#else
-      st_plain(x + i, xv + ycoef * vn);
-#endif
+      st_kind<TPL_WT_X>(x + i, xv + ycoef * vn);
     }
     if (Vcol) Vcol[i] = vn;
     return vn;

@@ -212,9 +212,17 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     double2 r;
     r.x = w.x - alpha * (rc.x * invN);
     r.y = w.y - alpha * (rc.y * invN);
-#if TPL_WT_AXPY
+#if TPL_WT_AXPY == 1
     st_out(r_next + i0, r.x);
     if (i0 + 1 < end) st_out(r_next + i0 + 1, r.y);
+#elif TPL_WT_AXPY == 2
+    if (i0 + 1 < end) {
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      d2v rv = {r.x, r.y};
+      __builtin_nontemporal_store(rv, reinterpret_cast<d2v*>(r_next + i0));
+    } else {
+      __builtin_nontemporal_store(r.x, r_next + i0);
+    }
 #else
     if (i0 + 1 < end) {
       *reinterpret_cast<double2*>(r_next + i0) = r;
