@@ -190,7 +190,10 @@ __device__ __forceinline__ double finish_partials_wave(int N, const PartialRegs<
 #define TPL_WT_STORES 1
 #endif
 #ifndef TPL_WT_AXPY
-#define TPL_WT_AXPY 0  // r_{j+1} of k_p1_axpy: 16-B plain stores (measured faster)
+// r_{j+1} of k_p1_axpy: 16-B non-temporal stores. Same box, alternated twice (r03):
+// solve 9.50-9.56 vs 9.59 ms with plain 16-B stores, pass one 12.16-12.22 vs 12.33-12.34 us
+// per step, k_p1_axpy 3.72 vs 3.83 us isolated; write-through (1) measured +0.5 us (r02)
+#define TPL_WT_AXPY 2
 #endif
 #ifndef TPL_WT_W
 #define TPL_WT_W 1  // pass one's w (read next by k_p1_axpy on the same XCD only)
