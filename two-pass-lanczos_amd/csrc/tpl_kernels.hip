@@ -181,13 +181,24 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   // `end` is always readable); the loads are unconditional so none is sunk behind the
   // reduction.
   constexpr int kAxPairs = 4;
+#ifndef TPL_NT_WLOAD
+#define TPL_NT_WLOAD 0  // lab: non-temporal loads of w (its last use)
+#endif
   const int64_t i00 = beg + 2 * threadIdx.x;
   double2 w0[kAxPairs], rc0[kAxPairs];
 #pragma unroll
   for (int q = 0; q < kAxPairs; ++q) {
     const int64_t i0 = i00 + (int64_t)q * 2 * kTPB;
     const int64_t ic = i0 < end ? i0 : beg;
+#if TPL_NT_WLOAD
+    {
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(W + ic));
+      w0[q] = double2(t.x, t.y);
+    }
+#else
     w0[q] = *reinterpret_cast<const double2*>(W + ic);
+#endif
     rc0[q] = *reinterpret_cast<const double2*>(r_cur + ic);
   }
   // The DevState scalars (stop flag, ||r_j||) are read only now, with the vector loads
