@@ -49,6 +49,16 @@ ARCS_SCALE = 5000000   # BASELINE configs[4]
 # test_headline_pinned_order_bitwise checks that exact operator against the oracle.
 PINNED_ORDER_GROUPS = {500000: 13}
 ORACLE_CFLAGS = "gcc 11 -O2 -mfma -ffp-contract=off -fno-fast-math (oracle/Makefile)"
+# Expected digests of every timed workload, computed on the CPU by the oracle in the
+# device's reduction order (tests/golden/make_parity.py; pinned by
+# tests/test_parity_digests.py): the `parity` block compares the GPU's results with them
+PARITY_FILE = os.path.join(ROOT, "tests", "golden", "parity.json")
+# configs[1] (f = exp on the device: a tolerance, not bits) against the reference-order
+# oracle with LAPACK's exp (SURVEY.md §0.5 measured 1.2e-14 between orders)
+EXP_TOL = 1e-10
+# N > 1: the parent's limit on the whole torchrun child (then it kills the child's
+# process group and reports the last stage every rank reached)
+CHILD_TIMEOUT_S = 900
 
 
 def parse(argv=None):
@@ -92,6 +102,10 @@ def parse(argv=None):
                    help="N=1: also time BASELINE configs[3] (one-pass k with CGS2 "
                         "re-orthogonalisation, V_k in HBM); 0 to skip")
     p.add_argument("--pcie", type=int, default=1, help="N=1: also time host b / x (PCIe)")
+    p.add_argument("--parity", type=int, default=1,
+                   help="0 to skip the parity block (digests vs tests/golden/parity.json)")
+    p.add_argument("--child-timeout", type=float, default=CHILD_TIMEOUT_S,
+                   help="N>1: seconds the parent waits for the torchrun child")
     return p.parse_args(argv)
 
 
@@ -150,12 +164,141 @@ def time_solves(solve, reps: int, sync) -> float:
     return (time.perf_counter() - t) / reps
 
 
-def x_digest(x) -> str:
-    """First 16 hex digits of sha256 over x's fp64 bytes (bit-identity across runs)."""
+def x_digest(*arrays) -> str:
+    """First 16 hex digits of sha256 over the fp64 bytes of the arrays, in order (bit
+    identity across runs; the rule of tests/golden/make_parity.py)."""
     import hashlib
 
     import numpy as np
-    return hashlib.sha256(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest()[:16]
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a, dtype=np.float64).tobytes())
+    return h.hexdigest()[:16]
+
+
+def expected_parity() -> dict:
+    try:
+        with open(PARITY_FILE) as f:
+            return json.load(f)["workloads"]
+    except (OSError, ValueError, KeyError):
+        return {}
+
+
+def parity_entry(expected: dict, name: str, **got) -> dict:
+    """One workload's verdict: each digest `got` (x / coef) against the committed one."""
+    exp = expected.get(name)
+    if exp is None:
+        return {"ok": False, "error": f"no committed expectation for {name!r}"}
+    ent = {}
+    ok = True
+    for key, val in got.items():
+        ent[key] = val
+        ent[key + "_expected"] = exp.get(key)
+        ok = ok and val == exp.get(key)
+    ent["ok"] = ok
+    return ent
+
+
+def rocprof_spmv(steps: int, b_spmv: float):
+    """In-graph average duration of both SpMV kernels from the committed rocprofv3 summary
+    of the headline (profiles/rocprof_headline.json, scripts/update_profiles.py): their
+    fractions of the HBM roofline by B_spmv, and the time-weighted one over all 2k - 1
+    SpMV launches of a solve (k of k_p1_spmv, k - 1 of k_p2_spmv)."""
+    path = os.path.join(ROOT, "profiles", "rocprof_headline.json")
+    try:
+        with open(path) as f:
+            rj = json.load(f)
+        t1, t2 = float(rj["avg_ns"]["k_p1_spmv"]), float(rj["avg_ns"]["k_p2_spmv"])
+    except (OSError, ValueError, KeyError):
+        return None
+    frac = lambda ns: round(b_spmv / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
+    tw = (2 * steps - 1) * b_spmv / ((steps * t1 + (steps - 1) * t2) * 1e-9) / 1e9 / HBM_PEAK_GBS
+    return {"k_p1_spmv": {"avg_us": round(t1 / 1000, 3), "frac": frac(t1)},
+            "k_p2_spmv": {"avg_us": round(t2 / 1000, 3), "frac": frac(t2)},
+            "all_spmv_time_weighted_frac": round(tw, 4), "source": rj.get("source")}
+
+
+# ---- N > 1: the parent process (never touches the GPU) ------------------------------
+def stage_marker(stage: str) -> None:
+    """Append this rank's progress to its marker file (TPL_BENCH_STAGE_DIR, set by the
+    parent), so a hung or failed N-rank run still reports where every rank stopped."""
+    d = os.environ.get("TPL_BENCH_STAGE_DIR")
+    if not d:
+        return
+    try:
+        with open(os.path.join(d, f"rank{os.environ.get('RANK', '0')}.stage"), "a") as f:
+            f.write(f"{time.time():.3f} {os.getpid()} {stage}\n")
+    except OSError:
+        pass
+
+
+def read_stages(d: str) -> dict:
+    """rank -> {"stage": last stage, "t": seconds since the parent started it}."""
+    out = {}
+    try:
+        names = sorted(os.listdir(d))
+    except OSError:
+        return out
+    for fn in names:
+        if not fn.endswith(".stage"):
+            continue
+        try:
+            with open(os.path.join(d, fn)) as f:
+                lines = [ln.split(" ", 2) for ln in f.read().splitlines() if ln.strip()]
+        except OSError:
+            continue
+        if lines and all(len(ln) == 3 for ln in lines):
+            out[fn[len("rank"):-len(".stage")]] = {"stage": lines[-1][2], "stages": len(lines),
+                                                   "t": float(lines[-1][0]),
+                                                   "pid": int(lines[-1][1])}
+    return out
+
+
+def run_parent(argv, nproc: int, timeout: float, cmd=None) -> int:
+    """Launch the N-rank child (torchrun; `cmd` overrides it for tests) in its own process
+    group, wait at most `timeout` s; on a time-out or a failure kill the whole group and
+    print ONE JSON line naming the last stage each rank reached. Returns the exit status."""
+    import signal
+    import tempfile
+    d = tempfile.mkdtemp(prefix="tpl_bench_stages_")
+    env = dict(os.environ, TPL_BENCH_STAGE_DIR=d)
+    cmd = cmd or launch_command(argv, nproc, _free_port())
+    t0 = time.time()
+    p = subprocess.Popen(cmd, env=env, start_new_session=True)
+    status, rc = "ok", 0
+    try:
+        rc = p.wait(timeout=timeout)
+        if rc != 0:
+            status = "failed"
+    except subprocess.TimeoutExpired:
+        status, rc = "timeout", 124
+    if status != "ok":
+        # torchrun forwards SIGTERM to its workers (each in a session of its own); then
+        # SIGKILL the launcher's group and every rank pid the markers recorded
+        for sig in (signal.SIGTERM, signal.SIGKILL):
+            try:
+                os.killpg(p.pid, sig)
+            except ProcessLookupError:
+                break
+            try:
+                p.wait(timeout=30)
+                break
+            except subprocess.TimeoutExpired:
+                continue
+        stages = read_stages(d)
+        for st in stages.values():
+            try:
+                os.kill(st["pid"], signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
+            st["t"] = round(st["t"] - t0, 1)
+            del st["pid"]
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "Lanczos iterations/s",
+                          "n_gpus": nproc, "higher_is_better": True, "status": status,
+                          "exit_code": rc, "child_timeout_s": timeout,
+                          "wall_s": round(time.time() - t0, 1),
+                          "ranks_reporting": len(stages), "last_stage": stages}), flush=True)
+    return rc
 
 
 def main():
@@ -164,16 +307,19 @@ def main():
         args.other_configs = args.one_pass = args.pcie = args.scale_ref = 0
         args.cpu_baseline = args.single_ref = 0
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # parent of the N ranks: no GPU call here, no exec — a child, then its status
-        sys.exit(subprocess.call(launch_command(sys.argv[1:], args.gpus, _free_port())))
+        # parent of the N ranks: no GPU call here, no exec — a child under a time limit,
+        # then its status (or a JSON line naming where every rank stopped)
+        sys.exit(run_parent(sys.argv[1:], args.gpus, args.child_timeout))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    stage_marker("start")
     if world > 1:
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo")  # barriers / max-reduce of host timings only
+        stage_marker("process_group")
 
     import ctypes
 
@@ -217,8 +363,10 @@ def main():
         from tpl_amd.dist import DistContext, DistHipCsrOp
         dctx = DistContext(rank, world, device=device,
                            transport=os.environ.get("TPL_DIST_TRANSPORT", "rccl"))
+        stage_marker("comm_init")
         op = DistHipCsrOp(a, dctx)
         b_loc = op.local(b)
+    stage_marker("operator")
     b_dev = torch.from_numpy(np.ascontiguousarray(b_loc)).cuda(device)
     x_dev = torch.empty_like(b_dev)
     torch.cuda.synchronize()
@@ -232,8 +380,10 @@ def main():
                                         _lib.TPL_MEM_DEVICE))
 
     op.enable_timing(True)  # event records inside the captured passes (live timing)
+    stage_marker("first_solve (graph capture)")
     for _ in range(max(args.warmup, 0)):
         solve()
+    stage_marker("warmup_done")
     dec = tpl_amd.algorithms.lanczos_pass_one(op, b_loc, args.k)
     steps_taken = dec.steps_taken
 
@@ -243,6 +393,7 @@ def main():
             dist.barrier()
 
     barrier()
+    stage_marker("timed_loop")
     t0 = time.perf_counter()
     per_solve = []
     for _ in range(args.steps):
@@ -253,6 +404,7 @@ def main():
         per_solve.append(time.perf_counter() - ts)
     barrier()
     dt = time.perf_counter() - t0
+    stage_marker("timed_done")
     if dist is not None:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -292,6 +444,14 @@ def main():
     iters = args.steps * steps_taken
     value = iters / dt
     x_host = x_dev.cpu().numpy()
+    # parity: every timed workload's result against the digest the CPU oracle computed
+    # in the device's reduction order (tests/golden/parity.json), outside the timed region
+    expected = expected_parity() if args.parity else {}
+    parity = {}
+    if args.parity and not partitioned and (arcs, args.k, args.f) == (500000, 500, "inv") \
+            and op.order_groups() == PINNED_ORDER_GROUPS[500000]:
+        parity["headline"] = parity_entry(expected, "headline", x=x_digest(x_host),
+                                          coef=x_digest(dec.alphas, dec.betas))
     per_ms = sorted(1000.0 * t for t in per_solve)
     med_ms = per_ms[len(per_ms) // 2] if len(per_ms) % 2 else 0.5 * (per_ms[len(per_ms) // 2 - 1]
                                                                       + per_ms[len(per_ms) // 2])
@@ -310,6 +470,9 @@ def main():
             x_full = np.zeros(n)
             for rows, xs in parts:
                 x_full[rows] = xs
+            if args.parity and (arcs, args.k, args.f) == (ARCS_SCALE, 500, "inv"):
+                parity[f"configs4_{op.mode}_N{world}"] = parity_entry(
+                    expected, f"configs4_{op.mode}_N{world}", x=x_digest(x_full))
     if partitioned and args.single_ref:
         # the same workload on rank 0's GPU alone, for the speed-up of the partition, and
         # the partitioned x checked against it
@@ -389,6 +552,9 @@ def main():
                      "kernels_us_isolated": iso},
     }
 
+    rp = rocprof_spmv(steps_taken, b_spmv) if (arcs == 500000 and not partitioned) else None
+    if rp is not None:
+        out["roofline"]["spmv_kernels_rocprof"] = rp
     if single is not None:
         out["single_gpu_same_workload"] = single
     if partitioned:
@@ -434,11 +600,39 @@ def main():
                                             al.ctypes.data_as(PD), be.ctypes.data_as(PD),
                                             ctypes.byref(st), ctypes.byref(bn), None,
                                             _lib.TPL_MEM_DEVICE, reorth, None, None))
-        tm, second = {}, {}
+        tm, second, coef = {}, {}, {}
         for r in (0, 1, 2):
             tm[r] = time_solves(lambda: one_pass(r), 2, torch.cuda.synchronize)
             second[r] = op.reorth_second_passes()
+            coef[r] = x_digest(al[:st.value], be[:max(int(st.value) - 1, 0)])
         s1 = int(st.value)
+        if args.parity and args.k == 500 and op.order_groups() == PINNED_ORDER_GROUPS.get(arcs):
+            # configs[3]: solvers::lanczos (x = ||b|| V_k y') bit for bit; the CGS2 and
+            # selective runs by their coefficients, plus ||I - V^T V||_F of the basis
+            # (computed on the device: the north star's orthonormality check)
+            x1p = torch.empty_like(b_dev)
+            check(_lib.tpl_lanczos(op.handle, b_dev.data_ptr(), nloc, args.k, _lib.FTK_INV_PTR,
+                                   None, x1p.data_ptr(), _lib.TPL_MEM_DEVICE))
+            parity["configs3_one_pass"] = parity_entry(expected, "configs3_one_pass",
+                                                       x=x_digest(x1p.cpu().numpy()))
+            del x1p
+            for r, name in ((1, "configs3_cgs2"), (2, "configs3_selective")):
+                V = torch.empty((args.k, nloc), dtype=torch.float64, device=b_dev.device)
+                check(_lib.tpl_lanczos_standard(op.handle, b_dev.data_ptr(), nloc, args.k,
+                                                al.ctypes.data_as(PD), be.ctypes.data_as(PD),
+                                                ctypes.byref(st), ctypes.byref(bn), V.data_ptr(),
+                                                _lib.TPL_MEM_DEVICE, r, None, None))
+                sv = int(st.value)
+                V = V[:sv]
+                loss = float(torch.linalg.norm(torch.eye(sv, dtype=torch.float64, device=V.device)
+                                               - V @ V.T))
+                ent = parity_entry(expected, name, coef=coef[r])
+                ent["ortho_loss_fro"] = loss
+                ent["ortho_ok"] = loss < 1e-12  # 1.9e-14 measured in numpy
+                ent["ok"] = ent["ok"] and ent["ortho_ok"]
+                parity[name] = ent
+                del V
+                torch.cuda.empty_cache()
         rb = sum(2.0 * (16.0 * n * j + 24.0 * n) for j in range(1, s1))
         rate = rb / max(tm[1] - tm[0], 1e-9) / 1e9
         out["one_pass_reorth"] = {
@@ -456,6 +650,7 @@ def main():
             "ms_per_solve": round(1000 * tm[2], 2), "iterations_per_s": round(s1 / tm[2], 1),
             "second_passes": second[2], "steps": s1,
             "reorth_GBs": round(rate2, 1), "reorth_frac_of_hbm": round(rate2 / HBM_PEAK_GBS, 4)}
+    exp_case = None  # configs[1]: (A, b, device x), checked in the CPU leg
     if world == 1 and not partitioned and args.other_configs:
         # BASELINE configs[0] and [1] on the same GPU (parity-test sizes; reported, not `value`)
         others = {}
@@ -475,6 +670,10 @@ def main():
             others[f"{arcs_o}-arc k={k_o} f={f_o}"] = {
                 "ms_per_solve": round(1000 * dto, 3), "iterations_per_s": round(k_o / dto, 1),
                 "n": no, "nnz": int(ao.nnz)}
+            if args.parity and f_o == "inv":
+                parity["configs0"] = parity_entry(expected, "configs0", x=x_digest(xo.cpu().numpy()))
+            elif args.parity:
+                exp_case = (ao, bo.cpu().numpy(), xo.cpu().numpy(), k_o)
             opo.close()
         out["other_configs"] = others
     if world == 1 and not partitioned and args.scale_ref:
@@ -493,6 +692,9 @@ def main():
                                             _lib.TPL_MEM_DEVICE))
         op5.enable_timing(True)
         d5 = time_solves(solve5, 3, torch.cuda.synchronize)
+        if args.parity and args.k == 500:
+            parity["configs4_1gpu"] = parity_entry(expected, "configs4_1gpu",
+                                                   x=x_digest(x5.cpu().numpy()))
         q1, q2, qn = op5.pass_timing()
         u5 = q2 / qn
         out["configs4_5m_1gpu"] = {
@@ -534,7 +736,28 @@ def main():
             "loadavg_before_after": [round(load0[0], 2), round(load1[0], 2)],
             "compiler": ORACLE_CFLAGS, **host_info()}
         out["speedup_vs_cpu"] = round(value / (kc / tc), 1)
+        if exp_case is not None:
+            # configs[1]: the device exp is held to a tolerance (an EVD-class evaluation,
+            # not the host QL's bits): x against the reference-order oracle with LAPACK's
+            # exp
+            ae, be_, xe, ke = exp_case
+            oracle.set_threads(min(16, len(mask)))
+            xf = oracle.Operator(ae).lanczos_two_pass(be_, ke, ftk_ref.exp)
+            rel = float(np.linalg.norm(xe - xf) / np.linalg.norm(xf))
+            parity["configs1_exp"] = {"rel_err_vs_reference_order": rel, "tol": EXP_TOL,
+                                      "ok": rel <= EXP_TOL}
+    elif exp_case is not None:
+        parity["configs1_exp"] = {"ok": None, "skipped": "needs the CPU leg (--cpu-baseline 1)"}
+    if rank == 0 and parity:
+        out["parity"] = {
+            "all_ok": all(v.get("ok") is True for v in parity.values()),
+            "checked": len(parity),
+            "source": "tests/golden/parity.json: the CPU oracle in the device's reduction "
+                      "order (tests/golden/make_parity.py, pinned by "
+                      "tests/test_parity_digests.py)",
+            "workloads": parity}
     if rank == 0:
+        stage_marker("report")
         print(json.dumps(out), flush=True)
     op.close()
     if dctx is not None:

@@ -279,10 +279,14 @@ typedef struct tpl_csr_host {
 tpl_status tpl_load_kkt_system(const char* dmx_path, const char* qfc_path, tpl_csr_host* out);
 void tpl_csr_host_free(tpl_csr_host* csr);
 /* Synthetic KKT instance for the scale-out config (BASELINE.json configs[4]; the
- * reference has no generator at that size): num_arcs arcs (u, v), u != v, endpoints
- * uniform from a splitmix64 stream seeded by `seed`, ordered by (tail, head) like
- * netgen output, D empty (the 3-line qfc case), assembled exactly as
- * tpl_load_kkt_system assembles a parsed .dmx. num_nodes for a given m follows
+ * reference's netgen stops at 1.1M arcs, data/netgen/src/netgen.h:69-70): num_arcs arcs
+ * (u, v), u != v, from a splitmix64 stream seeded by `seed`, with the netgen instances'
+ * degree spread: each node draws an integer out-weight in [100, 1900]
+ * and in-weight in [800, 1200]; tails are drawn in proportion to out-weight, heads to
+ * in-weight (total degree / mean ~0.44 .. 1.58 at 5M arcs, like netgen's 0.5 .. 1.57 at
+ * 500k). Ordered by (tail, head) like netgen output, D empty (the 3-line qfc case),
+ * assembled exactly as tpl_load_kkt_system assembles a parsed .dmx; the same on every
+ * platform (integer arithmetic only). num_nodes for a given m follows
  * data/qcnd/pargen.c:41-50: floor((1 + sqrt(1 + 8m/0.75)) / 2).              */
 tpl_status tpl_generate_kkt(int64_t num_arcs, int64_t num_nodes, uint64_t seed,
                             tpl_csr_host* out);
@@ -371,6 +375,22 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
                                          tpl_op_t* out);
 /* Global row index of each entry of this operator's vectors (tpl_op_nrows entries). */
 tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows);
+
+/* ---- host-only plans (no GPU): the reduction order an operator would hold --------
+ * The host half of tpl_op_create_csr (mode TPL_PLAN_SINGLE: auto locality order, its
+ * group count pinned by order_groups > 0 as tpl_op_set_order_groups does; nranks 1,
+ * rank 0), of tpl_dist_op_create_replicated (TPL_PLAN_REPLICATED) or of a row-block
+ * rank with the tpl_dist_partition split (TPL_PLAN_ROWS), run by the same code: rank
+ * `rank` of `nranks`, its rows, order and SpMV layout, and nothing on a device. Only
+ * the host introspection calls accept the returned handle — tpl_op_nrows, tpl_op_nnz,
+ * tpl_op_flags, tpl_op_schedule, tpl_op_slices, tpl_op_permutation, tpl_op_local_rows,
+ * tpl_op_order_groups, tpl_kernel_algo_bytes — every other call returns
+ * TPL_ERR_INVALID_ARGUMENT; free it with tpl_op_destroy. The parity fixtures use it to
+ * restate a run's reduction order on a host without a GPU (tests/golden/make_parity.py). */
+enum { TPL_PLAN_SINGLE = 0, TPL_PLAN_REPLICATED = 1, TPL_PLAN_ROWS = 2 };
+tpl_status tpl_plan_create(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
+                           const double* vals, int mode, int nranks, int rank,
+                           int32_t order_groups, tpl_op_t* out);
 
 /* Kernel ids for tpl_profile_kernel */
 enum {

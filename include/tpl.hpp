@@ -23,6 +23,7 @@
 #ifndef TPL_HPP_
 #define TPL_HPP_
 
+#include <algorithm>
 #include <cstdint>
 #include <cstring>
 #include <exception>
@@ -224,8 +225,8 @@ class HipCsrOp {
  public:
   HipCsrOp(const Context& ctx, int64_t n, const std::vector<int64_t>& row_ptr,
            const std::vector<int32_t>& col_idx, const std::vector<double>& vals) {
-    if ((int64_t)row_ptr.size() != n + 1 || col_idx.size() != vals.size() ||
-        (int64_t)col_idx.size() != row_ptr.back())
+    if (n < 0 || (int64_t)row_ptr.size() != n + 1 || col_idx.size() != vals.size() ||
+        (int64_t)col_idx.size() != row_ptr.back())  // row_ptr has n + 1 >= 1 entries here
       throw EngineError(TPL_ERR_INVALID_ARGUMENT, "CSR arrays do not match n / nnz");
     detail::check(tpl_op_create_csr(ctx.handle(), n, (int64_t)vals.size(), row_ptr.data(),
                                     col_idx.data(), vals.data(), &op_));
@@ -304,7 +305,10 @@ struct Builtin {
   }
 };
 inline FtkSolver inv() { return Builtin{tpl_ftk_inv}; }  // T_k^{-1} e_1 (tridiagonal LU, partial pivoting)
-inline FtkSolver exp() { return Builtin{tpl_ftk_exp}; }  // exp(T_k) e_1 (symmetric tridiagonal QL)
+// exp(T_k) e_1: on the host a symmetric tridiagonal QL; as a solver's built-in it may run on
+// the device instead (a Chebyshev expansion within an EVD-class tolerance of the QL result,
+// include/tpl.h tpl_op_set_device_ftk) — tpl_op_set_device_ftk(op, 0) forces the host QL
+inline FtkSolver exp() { return Builtin{tpl_ftk_exp}; }
 inline FtkSolver sq() { return Builtin{tpl_ftk_sq}; }    // T_k^2 e_1
 }  // namespace ftk
 

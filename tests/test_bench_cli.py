@@ -28,18 +28,79 @@ def test_launch_command_shape():
 
 @pytest.mark.parametrize("rc", [0, 3])
 def test_parent_launches_ranks_as_child(monkeypatch, rc):
-    """--gpus N without WORLD_SIZE: bench.main() runs the launcher via subprocess.call
+    """--gpus N without WORLD_SIZE: bench.main() runs the launcher as a child (run_parent)
     and exits with the child's status before importing torch.cuda / touching a GPU."""
     seen = {}
     monkeypatch.delenv("WORLD_SIZE", raising=False)
     monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "1"])
-    monkeypatch.setattr(bench.subprocess, "call", lambda cmd: seen.setdefault("cmd", cmd) and rc)
+
+    def fake_parent(argv, nproc, timeout, cmd=None):
+        seen.update(cmd=bench.launch_command(argv, nproc, 1), timeout=timeout)
+        return rc
+    monkeypatch.setattr(bench, "run_parent", fake_parent)
     monkeypatch.setattr(bench.os, "execv", lambda *a: pytest.fail("exec"), raising=False)
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert e.value.code == rc
     assert "--nproc-per-node=2" in seen["cmd"]
     assert seen["cmd"][-4:] == ["--gpus", "2", "--steps", "1"]
+    assert seen["timeout"] == bench.CHILD_TIMEOUT_S
+
+
+# a stub of the N-rank child: two "ranks" that write stage markers as bench.main() does,
+# then either finish, fail, or hang past the parent's limit
+_STUB = r"""
+import os, subprocess, sys, time
+mode = sys.argv[1]
+if len(sys.argv) == 2:  # the launcher: start two ranks in sessions of their own (torchrun)
+    ps = [subprocess.Popen([sys.executable, __file__, mode, str(r)], start_new_session=True,
+                           env=dict(os.environ, RANK=str(r))) for r in range(2)]
+    sys.exit(max(p.wait() for p in ps))
+sys.path.insert(0, os.environ["BENCH_ROOT"])
+import bench
+r = int(sys.argv[2])
+bench.stage_marker("start")
+bench.stage_marker("comm_init")
+if mode == "ok":
+    sys.exit(0)
+if mode == "fail":
+    sys.exit(3 if r == 1 else 0)
+if r == 0:
+    bench.stage_marker("timed_loop")
+time.sleep(600)  # hang (the parent kills it)
+"""
+
+
+@pytest.mark.parametrize("mode,rc,status", [("ok", 0, None), ("fail", 3, "failed"),
+                                            ("hang", 124, "timeout")])
+def test_parent_timeout_and_stage_report(tmp_path, capsys, monkeypatch, mode, rc, status):
+    """run_parent on a stub child: a clean child passes its status through silently; a
+    failing or hung child is killed (its process group and every rank pid) and the parent
+    prints ONE JSON line naming the last stage each rank reached."""
+    import json
+    import time
+    stub = tmp_path / "stub.py"
+    stub.write_text(_STUB)
+    monkeypatch.setenv("BENCH_ROOT", ROOT)
+    t = time.time()
+    got = bench.run_parent([], 2, 5.0, cmd=[sys.executable, str(stub), mode])
+    assert got == rc
+    assert time.time() - t < 60
+    out = capsys.readouterr().out.strip()
+    if status is None:
+        assert out == ""
+        return
+    line = json.loads(out.splitlines()[-1])
+    assert line["status"] == status and line["n_gpus"] == 2 and line["value"] is None
+    assert line["metric"] == bench.METRIC
+    st = line["last_stage"]
+    if mode == "hang":
+        assert st["0"]["stage"] == "timed_loop" and st["1"]["stage"] == "comm_init"
+        assert line["ranks_reporting"] == 2
+    else:
+        assert st["1"]["stage"] == "comm_init"
+    for r in st.values():
+        assert "pid" not in r
 
 
 def test_rank_does_not_relaunch(monkeypatch):

@@ -118,6 +118,17 @@ def _check_partition_order(a, rs, mode, k):
     from partition_oracle import PartitionOracle
     import tpl_amd
     b = harness_b(a)
+    # the host-only plan (tpl_plan_create, what tests/golden/make_parity.py restates the
+    # bench's partitioned digests from) is the live rank's rows and layout
+    for r, rec in enumerate(rs):
+        plan = tpl_amd.HostPlan(a, mode=mode, nranks=len(rs), rank=r)
+        ps = plan.schedule()
+        assert np.array_equal(plan.local_rows, rec["rows"])
+        assert np.array_equal(ps["short_rows"], rec["s_short"])
+        assert np.array_equal(ps["long_rows"], rec["s_long"])
+        assert (ps["G2"], ps["E"], ps["slices"]) == (int(rec["s_G2"]), int(rec["s_E"]),
+                                                     int(rec["s_slices"]))
+        plan.close()
     po = PartitionOracle(a, rs, mode)
     al, be, s, bn = po.pass_one(b, k)
     assert int(rs[0]["steps"]) == s and float(rs[0]["bn"]) == bn

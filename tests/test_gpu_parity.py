@@ -565,6 +565,18 @@ def test_headline_pinned_order_bitwise(kkt_tmp):
     op2 = HipCsrOp(a)
     op2.set_order_groups(g)
     assert np.array_equal(solvers.lanczos_two_pass(op2, b, 500, ftk.INV), x)
+    # the host-only plan the parity fixture is made from holds this exact layout, and the
+    # fixture's digest is this x (tests/golden/make_parity.py, bench.py `parity`)
+    plan = tpl_amd.HostPlan(a, order_groups=g)
+    ps = plan.schedule()
+    for key in ("short_rows", "long_rows", "perm"):
+        assert np.array_equal(ps[key], sch[key]), key
+    assert (ps["G2"], ps["E"], ps["slices"]) == (sch["G2"], sch["E"], sch["slices"])
+    import json
+    import hashlib
+    with open(os.path.join(ROOT, "tests", "golden", "parity.json")) as f:
+        exp = json.load(f)["workloads"]["headline"]
+    assert hashlib.sha256(x.tobytes()).hexdigest()[:16] == exp["x"]
     op.close()
     op2.close()
 

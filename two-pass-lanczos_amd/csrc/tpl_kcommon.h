@@ -4,42 +4,9 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include "tpl_device.h"
+#include "tpl_lab.h"  // diagnostic stamp hooks (empty in the product build)
 
 namespace tpl {
-
-#ifndef TPL_STAMP
-#define TPL_STAMP 0
-#endif
-#ifndef TPL_PRE_LATE
-#define TPL_PRE_LATE 1  // chunk rows' own vector entries issued after the gathers (they are needed only
-                        // by the epilogue; issued first they delay the bins' critical loads)
-#endif
-#if TPL_STAMP
-// Diagnostic builds only: per-workgroup s_memrealtime (100 MHz) marks of the most
-// recent SpMV-shaped launch — [0] start, [1] scale known, [2] products staged /
-// row sums done, [3] piece sums staged, [4] publish drained, [5] end — read back
-// by tpl_debug_stamps().
-constexpr int kMarks = 7;  // marks 0..5 + the workgroup's HW_ID / XCC_ID in slot 6
-__device__ unsigned long long g_stamps[kMarks * 65536];
-__device__ int g_stamps_n;  // k_ftk_exp: the expansion's term count of the last launch
-#define TPL_MARK(k)                                                          \
-  do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x < 65536)                              \
-      g_stamps[kMarks * blockIdx.x + (k)] = __builtin_amdgcn_s_memrealtime(); \
-  } while (0)
-#define TPL_MARK_ID()                                                        \
-  do {                                                                       \
-    if (threadIdx.x == 0 && blockIdx.x < 65536) {                            \
-      unsigned hw_, xcc_;                                                    \
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw_));     \
-      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID, 0, 4)" : "=s"(xcc_)); \
-      g_stamps[kMarks * blockIdx.x + 6] = ((unsigned long long)xcc_ << 32) | hw_; \
-    }                                                                        \
-  } while (0)
-#else
-#define TPL_MARK(k) do {} while (0)
-#define TPL_MARK_ID() do {} while (0)
-#endif
 
 // ---------------------------------------------------------------- reductions
 // 64-bit lane exchange through a DPP pattern (two 32-bit moves).
@@ -153,88 +120,17 @@ __device__ __forceinline__ double finish_partials(const double* __restrict__ P, 
   return block_sum(s, red);
 }
 
-// The same canonical reduction computed by every wave on its own, for N <= 256 (one
-// partial per thread t of the tree): lane l holds s_t for the four threads t = l + 64u
-// (u = 0..3) of the four waves, four butterflies give the four wave totals, combined
-// as tree256 combines them — bit for bit the block result, without LDS or barriers (a
-// barrier in the middle of an SpMV waits for every wave's outstanding gathers).
-// wave_red selects the load pattern: lane-major for the wave reduction, else the
-// block pattern of load_partials (the choice is uniform per launch).
-template <int R>
-__device__ __forceinline__ void load_partials_sel(const double* __restrict__ P, int N,
-                                                  bool wave_red, PartialRegs<R>& r) {
-  const int l = threadIdx.x & 63;
-#pragma unroll
-  for (int u = 0; u < R; ++u)
-    r.v[u] = P[clampi(wave_red ? l + 64 * u : (int)threadIdx.x + u * kTPB, N - 1)];
-}
-template <int R>
-__device__ __forceinline__ double finish_partials_wave(int N, const PartialRegs<R>& r) {
-  static_assert(R >= 4, "four sub-waves");
-  const int l = threadIdx.x & 63;
-  double t[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    double s = 0.0;
-    if (l + 64 * u < N) s = s + r.v[u];
-    t[u] = wave_sum(s);
-  }
-  return (t[0] + t[1]) + (t[2] + t[3]);
-}
-
-// Vector results of a step (w, v_{j+1}, x, r_{j+1}) are consumed only by the NEXT
-// launch. Stored write-through (agent-scope relaxed stores: global_store ... sc1) they
-// leave the XCD's L2 while the kernel runs, instead of as dirty lines written back at
-// the kernel boundary (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s).
-#ifndef TPL_WT_STORES
-#define TPL_WT_STORES 1
-#endif
-#ifndef TPL_WT_AXPY
-// r_{j+1} of k_p1_axpy: 16-B non-temporal stores. Same box, alternated twice (r03):
-// solve 9.50-9.56 vs 9.59 ms with plain 16-B stores, pass one 12.16-12.22 vs 12.33-12.34 us
-// per step, k_p1_axpy 3.72 vs 3.83 us isolated; write-through (1) measured +0.5 us (r02)
-#define TPL_WT_AXPY 2
-#endif
-#ifndef TPL_WT_W
-#define TPL_WT_W 1  // pass one's w (read next by k_p1_axpy on the same XCD only)
-#endif
-#ifndef TPL_WT_V
-#define TPL_WT_V 1  // pass two's v_{j+1} (gathered by every XCD next step)
-#endif
-#ifndef TPL_WT_X
-#define TPL_WT_X 1  // pass two's x (read again three steps later, same XCD only)
-#endif
-__device__ __forceinline__ void st_plain(double* p, double v) { *p = v; }
+// Vector results of a step (w, v_{j+1}, x) are consumed only by the NEXT launch. Stored
+// write-through (agent-scope relaxed stores: global_store ... sc1) they leave the XCD's L2
+// while the kernel runs, instead of as dirty lines written back at the kernel boundary
+// (MI355X_MICROARCH.md "boundary": + dirty bytes / 6 TB/s). Measured against plain and
+// non-temporal stores for each of w, v_{j+1} and x (r02-r03, variant builds, same box,
+// alternated): write-through kept for all three. r_{j+1} (k_p1_axpy)
+// is the exception: 16-B non-temporal stores.
 __device__ __forceinline__ void st_out(double* p, double v) {
-#if TPL_WT_STORES
   __hip_atomic_store(reinterpret_cast<unsigned long long*>(p),
                      (unsigned long long)__double_as_longlong(v), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
-#else
-  *p = v;
-#endif
-}
-
-// Store flavour of a vector result: 0 plain, 1 write-through (st_out), 2 non-temporal
-// (lab variants only; the shipped flavours are the macros' defaults).
-template <int K>
-__device__ __forceinline__ void st_kind(double* p, double v) {
-  if constexpr (K == 2) __builtin_nontemporal_store(v, p);
-  else if constexpr (K == 1) st_out(p, v);
-  else st_plain(p, v);
-}
-
-// The previous basis vector's own-row load (its last use in the step): plain, or a
-// non-temporal hint (lab variant TPL_NT_PREV=1).
-#ifndef TPL_NT_PREV
-#define TPL_NT_PREV 0
-#endif
-__device__ __forceinline__ double ld_prev(const double* p) {
-#if TPL_NT_PREV
-  return __builtin_nontemporal_load(p);
-#else
-  return *p;
-#endif
 }
 
 // Pins a value as computed unconditionally: without it the compiler sinks the loads
@@ -268,7 +164,7 @@ struct EpiPass1 {
   double* W;
   double* Vcol;         // standard variant: column j-1 of V_k, else nullptr
   double* Pa_long;      // alpha partials of the long rows (Pa + n_chunks)
-  __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], ld_prev(r_prev + i)}; }
+  __device__ __forceinline__ Pre1 pre(int i) const { return Pre1{r_cur[i], r_prev[i]}; }
   // long row r: its alpha partial is the single rounded product v * w
   __device__ __forceinline__ void long_alpha(int r, double acc) const { st_out(Pa_long + r, acc); }
   // returns v_j[i]
@@ -276,7 +172,7 @@ struct EpiPass1 {
     const double v = p.rc * invN_cur;
     const double vp = has_prev ? p.rp * invN_prev : 0.0;
     const double w = s - beta_sub * vp;
-    st_kind<TPL_WT_W>(W + i, w);
+    st_out(W + i, w);
     if (Vcol) Vcol[i] = v;
     acc = fma(v, w, acc);
     return v;
@@ -289,68 +185,7 @@ struct EpiPass1 {
 // other, exactly as m separate steps would round them; nflush = 0 leaves x untouched.
 // The host flushes every third step and at the last one, so x is read and written once
 // per three steps instead of every step.
-struct Pre2 {
-  double vc, vp, x;
-};
-struct EpiPass2 {
-  const double* v_cur;
-  const double* v_prev; // == v_cur (never used) at j == 1 where v_0 = 0
-  bool has_prev;
-  int nflush;           // 0..3 x terms applied by this step
-  double beta_sub, alpha, invb, ycoef, ycoef1, ycoef2;  // y[j], y[j-1], y[j-2]
-  double* v_next;
-  double* x;
-  double* Vcol; // lanczos_pass_two_with_basis: column j of V'_k, else nullptr
-  __device__ __forceinline__ Pre2 pre(int i) const {
-    return Pre2{v_cur[i], ld_prev(v_prev + i), nflush ? x[i] : 0.0};
-  }
-  // returns v_{j+1}[i]
-  __device__ __forceinline__ double apply(int i, double s, const Pre2& p, double&) const {
-    const double vp = has_prev ? p.vp : 0.0;
-    double w = s - beta_sub * vp;
-    w = w - alpha * p.vc;
-    const double vn = w * invb;
-    st_kind<TPL_WT_V>(v_next + i, vn);
-    if (nflush) {
-      double xv = p.x;
-      if (nflush >= 3) xv = xv + ycoef2 * p.vp;
-      if (nflush >= 2) xv = xv + ycoef1 * p.vc;
-      st_kind<TPL_WT_X>(x + i, xv + ycoef * vn);
-    }
-    if (Vcol) Vcol[i] = vn;
-    return vn;
-  }
-  __device__ __forceinline__ void long_alpha(int, double) const {}
-};
-// Pointers (kernel arguments) only: usable before anything is loaded.
-__device__ __forceinline__ void p2_epi_ptrs(EpiPass2& epi, const double* v_cur, const double* v_prev,
-                                            double* v_next, double* x, double* Vcol, int j,
-                                            int nflush) {
-  epi.v_cur = v_cur;
-  epi.v_prev = (j >= 2) ? v_prev : v_cur;
-  epi.has_prev = j >= 2;
-  epi.nflush = nflush;
-  epi.v_next = v_next;
-  epi.x = x;
-  epi.Vcol = Vcol;
-}
-// The recurrence coefficients (DevState scalars, written by pass one / the host).
-__device__ __forceinline__ void p2_epi_coefs(EpiPass2& epi, const DevState& S, int j, int nflush) {
-  epi.beta_sub = (j >= 2) ? S.betas[j - 2] : 0.0;
-  epi.alpha = S.alphas[j - 1];
-  epi.invb = 1.0 / S.betas[j - 1];
-  epi.ycoef = S.y[j];
-  epi.ycoef1 = nflush >= 2 ? S.y[j - 1] : 0.0;
-  epi.ycoef2 = nflush >= 3 ? S.y[j - 2] : 0.0;
-}
-__device__ __forceinline__ void p2_epi_init(EpiPass2& epi, const DevState& S, const double* v_cur,
-                                            const double* v_prev, double* v_next, double* x,
-                                            double* Vcol, int j, int nflush) {
-  p2_epi_ptrs(epi, v_cur, v_prev, v_next, x, Vcol, j, nflush);
-  p2_epi_coefs(epi, S, j, nflush);
-}
-
-// pass two with the step's coefficients in a record (DevState::p2c, written by k_p2_coefs
+// The step's coefficients come in a record (DevState::p2c, written by k_p2_coefs
 // before the steps): record j = {beta_{j-1} (0 at j = 1), alpha_j, 1/beta_j, y_j, y_{j-1},
 // y_{j-2}, active, 0}. Lane l loads field l & 7 together with its row's own vector entries,
 // i.e. after the gathers, and the epilogue reads the fields with readlane. The unit gather
@@ -374,7 +209,7 @@ struct EpiPass2R {
   double* x;
   double* Vcol;
   __device__ __forceinline__ Pre2R pre(int i) const {
-    return Pre2R{v_cur[i], ld_prev(v_prev + i), nflush ? x[i] : 0.0, rec[threadIdx.x & 7]};
+    return Pre2R{v_cur[i], v_prev[i], nflush ? x[i] : 0.0, rec[threadIdx.x & 7]};
   }
   __device__ __forceinline__ double apply(int i, double s, const Pre2R& p, double&) const {
     if (readlane_f64(p.cv, 6) == 0.0) return 0.0;  // inactive launch (uniform)
@@ -384,12 +219,12 @@ struct EpiPass2R {
     double w = s - beta_sub * vp;
     w = w - alpha * p.vc;
     const double vn = w * invb;
-    st_kind<TPL_WT_V>(v_next + i, vn);
+    st_out(v_next + i, vn);
     if (nflush) {
       double xv = p.x;
       if (nflush >= 3) xv = xv + readlane_f64(p.cv, 5) * p.vp;
       if (nflush >= 2) xv = xv + readlane_f64(p.cv, 4) * p.vc;
-      st_kind<TPL_WT_X>(x + i, xv + ycoef * vn);
+      st_out(x + i, xv + ycoef * vn);
     }
     if (Vcol) Vcol[i] = vn;
     return vn;
@@ -410,7 +245,6 @@ __device__ __forceinline__ void pin_layout_args(const CsrDev& A) {
 // keep() for a row's epilogue inputs (used only for live rows / finalising threads)
 __device__ __forceinline__ void keep_pre(PreNone&) {}
 __device__ __forceinline__ void keep_pre(Pre1& p) { keep(p.rc); keep(p.rp); }
-__device__ __forceinline__ void keep_pre(Pre2& p) { keep(p.vc); keep(p.vp); keep(p.x); }
 __device__ __forceinline__ void keep_pre(Pre2R& p) { keep(p.vc); keep(p.vp); keep(p.x); keep(p.cv); }
 
 // Result of a workgroup's prologue: the gather scale, or "stop" (uniform across the grid).
@@ -543,10 +377,6 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
         a[q][k] = val_at<V8>(A.s_val, e);
       }
   }
-#if !TPL_PRE_LATE
-#pragma unroll
-  for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
-#endif
   if (WIN) {
 #pragma unroll
     for (int u = 0; u < kWinLoads; ++u)
@@ -562,10 +392,10 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
 #pragma unroll
       for (int k = 0; k < W; ++k) xv[q][k] = xsrc[c[q][k] < 0 ? 0 : c[q][k]];
   }
-#if TPL_PRE_LATE
+  // the rows' own vector entries after the gathers: needed only by the epilogue, issued
+  // first they delay the bins' critical loads
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
-#endif
   const Scale sc = scale_of();
   TPL_MARK(1);
   if (!sc.ok) return false; // stopped / breakdown (uniform)
@@ -803,18 +633,13 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
                                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("" ::: "memory");  // the slot loads stay behind the returned add
   if ((arrived & (unsigned)(ns - 1)) != (unsigned)(ns - 1)) return;
-#ifndef TPL_SLOT_LOADS
-#define TPL_SLOT_LOADS TPL_MAX_SLICES
-#endif
-#ifndef TPL_SLOT_WIDE
-#define TPL_SLOT_WIDE (TPL_SLOT_LOADS == 8)  // four 16-B loads (same box, alternated:
-#endif                                     // k_p2_spmv -0.1 us, pass one -0.15 us per step)
-  unsigned long long v[TPL_SLOT_LOADS];
-#if TPL_SLOT_WIDE
-  // 16-B sc1 loads of slot pairs (slot arrays are 64-B aligned). The four loads and their
-  // wait are ONE asm statement: the compiler must not touch the destination registers
-  // between the issue and the s_waitcnt (copying them early reads whatever they held).
-  static_assert(TPL_SLOT_LOADS == 8, "four pairs");
+  // 16-B sc1 loads of slot pairs (slot arrays are 64-B aligned): four instead of eight 8-B
+  // loads (same box, alternated: k_p2_spmv -0.1 us, pass one -0.15 us per step). The four
+  // loads and their wait are ONE asm statement: the compiler must not touch the destination
+  // registers between the issue and the s_waitcnt (copying them early reads whatever they
+  // held). Slots past the slice count re-read slot 0 (summed only up to ns).
+  static_assert(kSlices == 8, "four slot pairs");
+  unsigned long long v[kSlices];
   typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
   u64x2 r0, r1, r2, r3;
   const unsigned long long* p0 = slots;
@@ -832,14 +657,9 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
       : "memory");
   v[0] = r0.x; v[1] = r0.y; v[2] = r1.x; v[3] = r1.y;
   v[4] = r2.x; v[5] = r2.y; v[6] = r3.x; v[7] = r3.y;
-#else
-#pragma unroll
-  for (int k = 0; k < TPL_SLOT_LOADS; ++k)  // slots past the slice count: re-read slot 0
-    v[k] = __hip_atomic_load(slots + (k < ns ? k : 0), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
   double y = 0.0;
 #pragma unroll
-  for (int k = 0; k < TPL_SLOT_LOADS; ++k)
+  for (int k = 0; k < kSlices; ++k)
     if (k < ns) y = y + __longlong_as_double((long long)v[k]);
   if (A.long_defer) {  // partitioned: this rank's part of the row; finished after the exchange
     A.ypart[sg.ri] = y;
@@ -878,9 +698,7 @@ __device__ __forceinline__ int chunk_of_block(const CsrDev& A, int i) {
 }
 
 // Minimum waves per SIMD requested for the SpMV-shaped kernels (occupancy vs VGPRs).
-#ifndef TPL_SPMV_MIN_WAVES
-#define TPL_SPMV_MIN_WAVES 1
-#endif
+constexpr int kSpmvMinWaves = 1;
 // Grid: [bins of the long rows][short chunks] (or chunks first). Returns the chunk
 // index whose alpha partial this workgroup owns, or -1.
 // F = CW | V8 << 3 | SC16 << 4 | BC16 << 5 | WIN << 6: uniform chunk width (0: any), int8
@@ -915,15 +733,11 @@ template <int F, class Epi, class ScaleFn>
 __device__ __forceinline__ int spmv_block(const CsrDev& A, const double* __restrict__ xsrc,
                                           ScaleFn scale_of, const Epi& epi, double& acc,
                                           double* lds) {
-#if TPL_STAMP
   TPL_MARK(0);
   TPL_MARK_ID();
   const int r = spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
   TPL_MARK(5);
   return r;
-#else
-  return spmv_block_impl<F>(A, xsrc, scale_of, epi, acc, lds);
-#endif
 }
 
 } // namespace tpl

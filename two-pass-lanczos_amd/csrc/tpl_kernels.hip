@@ -33,7 +33,7 @@ namespace tpl {
 
 // ------------------------------------------------------------------ kernels
 template <int F>
-__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_spmv(CsrDev A, const double* __restrict__ x,
+__global__ __launch_bounds__(kTPB, kSpmvMinWaves) void k_spmv(CsrDev A, const double* __restrict__ x,
                                                double* __restrict__ y) {
   extern __shared__ double lds[];
   double acc = 0.0;
@@ -73,33 +73,32 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
 // Pass one / standard, step j >= 1. r_cur = r_j (== b at j = 1), this rank's rows;
 // xsrc = the gather source holding r_j for every column (== r_cur on one GPU, the
 // all-gathered vector when the rows are partitioned over ranks).
-// Occupancy of k_p1_spmv: its beta chain keeps values live across the whole SpMV (90 VGPRs
-// unconstrained: 5 waves per SIMD, so a 1,536-workgroup grid — 6 per CU at 500k arcs —
-// left 256 chunk workgroups waiting for a slot, chunk start median 2.1 us against 0.3 in
-// k_p2_spmv; scripts/stamps.py). The layouts with int8 values and narrow chunks (the KKT
-// ones) fit 6 waves per SIMD with no spill; the others would spill, so they keep the
-// default bound.
-#ifndef TPL_P1_WAVES
-#define TPL_P1_WAVES 6
-#endif
-constexpr int p1_min_waves(int F) {
-  return ((F & 8) && ((F & 7) == 1 || (F & 7) == 2)) ? TPL_P1_WAVES : TPL_SPMV_MIN_WAVES;
+// beta_{j-1} comes from the G2_r norm partials k_p1_axpy left: NBP per thread (1 when
+// G2_r <= 256, the usual case; 4 up to 1024), loaded at entry ahead of the entries and
+// gathers, reduced in scale_fn once they are in flight. The registers of those loads stay
+// live across the whole SpMV, so they set the kernel's occupancy: with one partial per
+// thread (the wave totals exchanged through LDS behind one barrier) k_p1_spmv<58> needs
+// 58 VGPRs, 8 waves per SIMD, and the 1,560-workgroup grid at 500k arcs is resident at
+// once; with four per lane (each wave reducing all 256 itself, no barrier: r03) it needed
+// 76 (6 waves): 24 workgroups waited for a slot and the chunks started at 1.8 us (median)
+// instead of 0.4 (stamps, scripts/stamps.py). Same box, alternated three times: solve
+// 9.12-9.17 vs 9.50-9.56 ms, pass one 11.35-11.45 vs 12.17-12.21 us per step, isolated
+// k_p1_spmv 6.60-6.67 vs 7.46-7.68 us; the tree and so the bits are the same.
+constexpr int p1_min_waves(int F, int NBP) {
+  return (NBP > 1 && (F & 8) && ((F & 7) == 1 || (F & 7) == 2)) ? 6 : kSpmvMinWaves;
 }
-template <int F>
-__global__ __launch_bounds__(kTPB, p1_min_waves(F)) void k_p1_spmv(CsrDev A, DevState S,
-                                                  const double* __restrict__ xsrc,
-                                                  const double* __restrict__ r_cur,
-                                                  const double* __restrict__ r_prev,
-                                                  double* __restrict__ W,
-                                                  double* __restrict__ Vcol, int j) {
-  __shared__ double red[4];
-  extern __shared__ double lds[];
+template <int F, int NBP>
+__device__ __forceinline__ void p1_spmv_body(const CsrDev& A, const DevState& S,
+                                             const double* __restrict__ xsrc,
+                                             const double* __restrict__ r_cur,
+                                             const double* __restrict__ r_prev,
+                                             double* __restrict__ W, double* __restrict__ Vcol,
+                                             int j, double* red, double* redb, double* lds) {
   pin_layout_args(A);
   asm volatile("" ::"s"(S.Pb_r), "s"(S.flags), "s"(S.norms), "s"(S.betas), "s"(S.Pa), "s"(A.G2_r),
                "s"(xsrc), "s"(r_cur), "s"(r_prev), "s"(W), "s"(Vcol), "s"(j));
-  PartialRegs<4> pr;           // G2 <= 1024
-  const bool wave_red = A.G2_r <= kTPB;  // beta reduced by each wave alone (no barrier)
-  load_partials_sel(S.Pb_r, A.G2_r, wave_red, pr);
+  PartialRegs<NBP> pr;
+  load_partials(S.Pb_r, A.G2_r, pr);
   // the stop flag and beta_{j-2} with the partials, ahead of the entries and gathers:
   // read later, their wait would drain every gather in flight before the beta chain
   int stop0 = S.flags[0];
@@ -126,8 +125,17 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F)) void k_p1_spmv(CsrDev A, Dev
     asm volatile("" : "+v"(stop0), "+v"(norm_prev));
     if (stop0) return Scale{0.0, false};
     epi.invN_prev = (j >= 2) ? 1.0 / norm_prev : 0.0;
-    const double beta = sqrt(wave_red ? finish_partials_wave(A.G2_r, pr)
-                                      : finish_partials(S.Pb_r, A.G2_r, pr, red));
+    // the canonical tree (s = 0; s += P[t + 256u]; tree256), one barrier: its LDS words
+    // (redb) are not reused, and the barrier waits for LDS traffic only, never for the
+    // gathers in flight
+    double beta;
+    if constexpr (NBP == 1) {
+      double sq = 0.0;
+      if ((int)threadIdx.x < A.G2_r) sq = sq + pr.v[0];
+      beta = sqrt(block_sum_tail(sq, redb));
+    } else {  // any count (more than 256 NBP in batches)
+      beta = sqrt(finish_partials(S.Pb_r, A.G2_r, pr, redb));
+    }
     if (beta <= kBreakdownTol) {
       // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
       // j  > 1: breakdown -> steps_taken = j - 1, beta not pushed
@@ -153,6 +161,31 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F)) void k_p1_spmv(CsrDev A, Dev
   // write-through: every k_p1_axpy workgroup, on every XCD, reads all the partials
   // next (measured: pass one -0.2 to -0.3 us per step against a plain store)
   if (threadIdx.x == 0) st_out(S.Pa + slot, p);
+}
+// G2_r <= 256 norm partials (one per thread) ...
+template <int F>
+__global__ __launch_bounds__(kTPB, p1_min_waves(F, 1)) void k_p1_spmv(CsrDev A, DevState S,
+                                                  const double* __restrict__ xsrc,
+                                                  const double* __restrict__ r_cur,
+                                                  const double* __restrict__ r_prev,
+                                                  double* __restrict__ W,
+                                                  double* __restrict__ Vcol, int j) {
+  __shared__ double red[4], redb[4];
+  extern __shared__ double lds[];
+  p1_spmv_body<F, 1>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
+}
+// ... and more (four per thread first, the rest in batches; the 5M-arc instance's 1,024
+// row blocks)
+template <int F>
+__global__ __launch_bounds__(kTPB, p1_min_waves(F, 4)) void k_p1_spmv_wide(CsrDev A, DevState S,
+                                                  const double* __restrict__ xsrc,
+                                                  const double* __restrict__ r_cur,
+                                                  const double* __restrict__ r_prev,
+                                                  double* __restrict__ W,
+                                                  double* __restrict__ Vcol, int j) {
+  __shared__ double red[4], redb[4];
+  extern __shared__ double lds[];
+  p1_spmv_body<F, 4>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
 }
 
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
@@ -181,24 +214,13 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   // `end` is always readable); the loads are unconditional so none is sunk behind the
   // reduction.
   constexpr int kAxPairs = 4;
-#ifndef TPL_NT_WLOAD
-#define TPL_NT_WLOAD 0  // lab: non-temporal loads of w (its last use)
-#endif
   const int64_t i00 = beg + 2 * threadIdx.x;
   double2 w0[kAxPairs], rc0[kAxPairs];
 #pragma unroll
   for (int q = 0; q < kAxPairs; ++q) {
     const int64_t i0 = i00 + (int64_t)q * 2 * kTPB;
     const int64_t ic = i0 < end ? i0 : beg;
-#if TPL_NT_WLOAD
-    {
-      typedef double d2v __attribute__((ext_vector_type(2)));
-      const d2v t = __builtin_nontemporal_load(reinterpret_cast<const d2v*>(W + ic));
-      w0[q] = double2(t.x, t.y);
-    }
-#else
     w0[q] = *reinterpret_cast<const double2*>(W + ic);
-#endif
     rc0[q] = *reinterpret_cast<const double2*>(r_cur + ic);
   }
   // The DevState scalars (stop flag, ||r_j||) are read only now, with the vector loads
@@ -223,10 +245,9 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     double2 r;
     r.x = w.x - alpha * (rc.x * invN);
     r.y = w.y - alpha * (rc.y * invN);
-#if TPL_WT_AXPY == 1
-    st_out(r_next + i0, r.x);
-    if (i0 + 1 < end) st_out(r_next + i0 + 1, r.y);
-#elif TPL_WT_AXPY == 2
+    // 16-B non-temporal stores: r_{j+1} leaves the L2 during the kernel instead of as
+    // 4 MB of dirty lines at the boundary (same box, alternated twice: pass one 12.16-12.22
+    // vs 12.33 us per step with plain 16-B stores; write-through +0.5 us)
     if (i0 + 1 < end) {
       typedef double d2v __attribute__((ext_vector_type(2)));
       d2v rv = {r.x, r.y};
@@ -234,13 +255,6 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     } else {
       __builtin_nontemporal_store(r.x, r_next + i0);
     }
-#else
-    if (i0 + 1 < end) {
-      *reinterpret_cast<double2*>(r_next + i0) = r;
-    } else {
-      r_next[i0] = r.x;
-    }
-#endif
     acc = i0 < A.norm_n ? fma(r.x, r.x, acc) : acc;
     acc = i0 + 1 < end && i0 + 1 < A.norm_n ? fma(r.y, r.y, acc) : acc;
   };
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(kTPB) void k_p2_init(int64_t n, DevState S,
 // coefficient record (EpiPass2R: loaded after the gathers, never waited on before the
 // epilogue; the gather scale is 1).
 template <int F>
-__global__ __launch_bounds__(kTPB, TPL_SPMV_MIN_WAVES) void k_p2_spmv(CsrDev A,
+__global__ __launch_bounds__(kTPB, kSpmvMinWaves) void k_p2_spmv(CsrDev A,
                                                   const double* __restrict__ rec,
                                                   const double* __restrict__ xsrc,
                                                   const double* __restrict__ v_cur,
@@ -696,9 +710,7 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S, int scale) {
     if (u < R && i < n) S.y[i] = (eb * yv[u]) * bnorm;
   }
   TPL_MARK(5);
-#if TPL_STAMP
-  if (t == 0) g_stamps_n = N;
-#endif
+  TPL_STAMP_TERMS(N);
 }
 
 // Row permutation at the boundary (locality order, tpl_layout.h): out[i] = in[idx[i]] for
@@ -766,9 +778,12 @@ __global__ __launch_bounds__(kTPB) void k_long_epi_p1(CsrDev A, DevState S,
     const int r = blockIdx.x - nbl;
     const double* P = yall + (size_t)r * A.y_ld + A.n_long;
     const int N = A.nch[r];
-    PartialRegs<8> pr;
-    load_partials(P, N, pr);
-    const double tot = finish_partials(P, N, pr, red);
+    double tot = 0.0;  // a rank without short rows (N == 0, uniform): nothing to load
+    if (N > 0) {
+      PartialRegs<8> pr;
+      load_partials(P, N, pr);
+      tot = finish_partials(P, N, pr, red);
+    }
     if (threadIdx.x == 0) Pa_long[r - R] = tot;
     return;
   }
@@ -1074,8 +1089,9 @@ hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStrea
 }
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
-  if (spmv_grid(A) > 0)
-    return TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
+  if (spmv_grid(A) <= 0) return hipGetLastError();
+  if (A.G2_r <= kTPB) return TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
+  return TPL_LAUNCH_CW(k_p1_spmv_wide, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
@@ -1183,12 +1199,3 @@ hipError_t reorth_decide(const DevState& S, const double* Pb1, int G2, int* skip
 
 } // namespace launch
 } // namespace tpl
-
-#if TPL_STAMP
-extern "C" int tpl_debug_stamps(unsigned long long* out, int n) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps), sizeof(unsigned long long) * tpl::kMarks * n);
-}
-extern "C" int tpl_debug_exp_terms(int* out) {
-  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps_n), sizeof(int));
-}
-#endif

@@ -26,6 +26,10 @@
 #include "tpl_internal.h"
 #include "tpl_layout.h"
 
+#ifndef TPL_LAB
+#define TPL_LAB 0  // lab builds only (scripts/build_variants.sh): runtime layout knobs
+#endif
+
 namespace tpl {
 namespace launch {
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
@@ -127,8 +131,9 @@ constexpr size_t kDevFtkMaxK = 1365;
 // (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
 // ~15-25 us (sync, host solve, upload, launch): one graph pays up to k ~ 128.
 constexpr size_t kDevFtkAutoK = 128;
-// The device exp (k_ftk_exp, a Chebyshev expansion: parallel over the rows of T_k) keeps 4 k
-// doubles in LDS (with its static arrays, under 64 KiB up to this k).
+// The device exp (k_ftk_exp, a Chebyshev expansion: parallel over the rows of T_k) keeps
+// 4 k + 4 doubles of dynamic LDS plus 8.2 KB of static arrays: 65.8 KB at this k, which
+// gfx950's 160 KiB of LDS per workgroup holds (a 64 KiB part would need k <= 1790).
 constexpr size_t kDevExpMaxK = 1800;
 // Which built-in f(T_k) a one-graph solve evaluates on the device.
 enum DevF { kDevInv = 0, kDevExp = 1 };
@@ -219,6 +224,10 @@ struct tpl_op_s {
   size_t vext_cols = 0;
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
+  // tpl_plan_create: the host half of an operator only (rows, order, layout), for the
+  // oracle's reduction order without a GPU; every device entry point refuses it
+  bool plan_only = false;
+  std::unique_ptr<tpl_dist_s> plan_dist;  // a plan's rank and rank count (no transport)
 };
 
 namespace {
@@ -325,15 +334,22 @@ void rebuild_schedule(tpl_op_s* op) {
   // 500k): window only in the caller's order.
   SchedParams sp = op->sp;
   sp.window = !p && !op->local_order;
-  if (const char* e = std::getenv("TPL_WINDOW")) sp.window = std::atoi(e) != 0;  // lab knob
-  if (const char* e = std::getenv("TPL_ELEM_ROWS")) sp.elem_rows = std::atoi(e);  // lab knob
-  if (const char* e = std::getenv("TPL_BIN_LINES")) sp.bin_lines = std::atoi(e);  // lab knob
-  if (const char* e = std::getenv("TPL_SLICES"))  // lab knob (auto slice count only)
-    if (sp.slices <= 0) sp.slices = std::atoi(e);
+#if TPL_LAB
+  // layout knobs of the lab builds (scripts/build_variants.sh -DTPL_LAB=1), never in the
+  // product library: the measured alternatives of DESIGN.md §3/§4
+  if (const char* e = std::getenv("TPL_WINDOW")) sp.window = std::atoi(e) != 0;
+  if (const char* e = std::getenv("TPL_ELEM_ROWS")) sp.elem_rows = std::atoi(e);
+  if (const char* e = std::getenv("TPL_BIN_LINES")) sp.bin_lines = std::atoi(e);
+  if (const char* e = std::getenv("TPL_SLICES")) {  // auto slice count only; the values
+    const int s = std::atoi(e);                     // tpl_op_set_slices accepts
+    if (sp.slices <= 0 && s > 0 && s <= kSlices && (s & (s - 1)) == 0) sp.slices = s;
+  }
+#endif
   // slice bounds over global columns — or, replicated-long-row partition, over this
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
                          p ? pcol : op->h_col, p ? pval : op->h_val, sp, cmap);
+  if (op->plan_only) return;  // tpl_plan_create: the layout is all a plan holds
   const Layout& L = op->lay;
   upload(op, &op->d_perm, op->perm);
   upload(op, &op->d_iperm, op->iperm);
@@ -436,7 +452,11 @@ void ensure_basis(tpl_op_s* op, size_t cols) {
   op->vcols = c;
 }
 
-void set_device(const tpl_op_s* op) { HIPCHK(hipSetDevice(op->device)); }
+void set_device(const tpl_op_s* op) {
+  if (op->plan_only)
+    fail(TPL_ERR_INVALID_ARGUMENT, "a host-only plan (tpl_plan_create) holds no device data");
+  HIPCHK(hipSetDevice(op->device));
+}
 
 void check_b(const tpl_op_s* op, const double* b, int64_t b_len) {
   if (!b && op->n > 0) fail(TPL_ERR_INVALID_ARGUMENT, "b is NULL");
@@ -851,7 +871,8 @@ void zero_out(tpl_op_s* op, double* x_out, int mem) {
 
 // Layout, vectors and events of a freshly filled operator (single GPU or one rank
 // of a partition; the vector stride ld is common to all ranks).
-void init_op(tpl_op_s* op) {
+// Vector stride ld, common to all ranks (the gathered vector holds rank r's block at r * ld).
+void set_stride(tpl_op_s* op) {
   const int R = op->dist && !op->hybrid ? op->dist->nranks : 1;  // gathered vector copies
   int64_t widest = op->n;
   if (op->dist && !op->hybrid)
@@ -860,6 +881,11 @@ void init_op(tpl_op_s* op) {
   // gathered column indices (ColMap: r * ld + local) are int32 on the device
   if ((int64_t)R * op->ld >= (int64_t)INT32_MAX)
     fail(TPL_ERR_UNSUPPORTED, "row blocks too unbalanced: nranks x widest block >= 2^31");
+}
+
+void init_op(tpl_op_s* op) {
+  const int R = op->dist && !op->hybrid ? op->dist->nranks : 1;  // gathered vector copies
+  set_stride(op);
   rebuild_schedule(op);
   // gathered: b, R0..2, V2_0..2, tmp (R x ld each); local: W, x (ld each)
   const size_t gathered = 8 * (size_t)R * op->ld, local = 2 * (size_t)op->ld;
@@ -896,7 +922,8 @@ void init_op(tpl_op_s* op) {
       const int32_t nmax = *std::max_element(op->nch.begin(), op->nch.end());
       op->y_ld1 = (int32_t)op->lay.lrows.size() + nmax;
       upload(op, &op->d_nch, op->nch);
-      const size_t ya = nr * (size_t)op->y_ld1;
+      // pass one strides the all-gather by y_ld1, pass two and tpl_op_apply by n_long + 1
+      const size_t ya = nr * (size_t)std::max<int64_t>(op->y_ld1, (int64_t)op->lay.lrows.size() + 1);
       dev_alloc(op, &op->d_yall, ya * sizeof(double));
       HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
     }
@@ -920,6 +947,110 @@ void balanced_cuts(const std::vector<double>& prefix, int nranks, int64_t* start
     i = starts[r];
   }
   starts[nranks] = m;
+}
+
+// Host half of tpl_dist_op_create_replicated (and of its tpl_plan_create): the short-row
+// split, this rank's rows in their order and its local CSR. op->n .. op->nch.
+void fill_replicated(tpl_op_s* op, int R, int me, int64_t n, const int64_t* row_ptr,
+                     const int32_t* col_idx, const double* vals) {
+  const int64_t nnz = row_ptr[n];
+  if (n < 1 || n >= INT32_MAX / 2 || nnz >= INT32_MAX || row_ptr[0] != 0)
+    fail(TPL_ERR_INVALID_ARGUMENT, "bad CSR sizes");
+  if (nnz > 0 && !vals) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+  check_csr(n, n, row_ptr, col_idx);
+  std::vector<int32_t> rp32(n + 1);
+  for (int64_t i = 0; i <= n; ++i) rp32[i] = (int32_t)row_ptr[i];
+  // short / long rows by the global rule; long rows are replicated on every rank
+  const int32_t T = short_row_threshold(n, rp32, -1);
+  std::vector<int64_t> S, Lr;
+  std::vector<int32_t> lidx(n, -1);
+  for (int64_t i = 0; i < n; ++i) {
+    if (rp32[i + 1] - rp32[i] > T) {
+      lidx[i] = (int32_t)Lr.size();
+      Lr.push_back(i);
+    } else {
+      S.push_back(i);
+    }
+  }
+  if ((int64_t)S.size() < R) fail(TPL_ERR_UNSUPPORTED, "fewer short rows than ranks");
+  // short rows in contiguous blocks balanced by bytes: the row itself plus the
+  // long-row entries in its column, which the owner of that column computes
+  std::vector<int32_t> longcnt(n, 0);
+  for (int64_t l : Lr)
+    for (int64_t q = row_ptr[l]; q < row_ptr[l + 1]; ++q) longcnt[col_idx[q]]++;
+  std::vector<double> prefix(S.size() + 1, 0.0);
+  for (size_t p = 0; p < S.size(); ++p) {
+    const int64_t i = S[p];
+    prefix[p + 1] = prefix[p] + 12.0 * (double)(rp32[i + 1] - rp32[i] + longcnt[i]) + 40.0;
+  }
+  std::vector<int64_t> cut(R + 1);
+  balanced_cuts(prefix, R, cut.data());
+  std::vector<int32_t> owner(n, -1);
+  for (int r = 0; r < R; ++r)
+    for (int64_t p = cut[r]; p < cut[r + 1]; ++p) owner[S[p]] = r;
+  // halo-free check (all ranks decide alike: they all see the whole matrix)
+  for (int64_t i : S)
+    for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+      const int32_t c = col_idx[q];
+      if (lidx[c] < 0 && owner[c] != owner[i])
+        fail(TPL_ERR_UNSUPPORTED, "a short row references a short row of another rank "
+                                  "(use the row-partitioned operator)");
+    }
+  op->hybrid = true;
+  op->n_glob = n;
+  const int64_t ns = cut[me + 1] - cut[me], nl = (int64_t)Lr.size();
+  op->ns_local = ns;
+  op->n = ns + nl;
+  // this rank's short rows; in the locality order (tpl_layout.h locality_order, the
+  // same key over the replicated long rows' ranks) when the rank's rows fit the auto
+  // rule. The local order is the caller's to follow through tpl_op_local_rows, so no
+  // vector is permuted on the device.
+  std::vector<int64_t> mine(S.begin() + cut[me], S.begin() + cut[me + 1]);
+  if (nl > 0 && op->n <= kReorderAutoMaxRows) {
+    // lidx is each long row's rank among the long rows, as locality_order ranks them
+    locality_sort(mine, row_ptr, col_idx, lidx.data(), (int32_t)nl, op->sp.order_groups);
+    op->local_order = true;
+  }
+  op->g2l.assign(n, -1);
+  op->local_rows.resize(op->n);
+  for (int64_t p = 0; p < ns; ++p) {
+    op->g2l[mine[p]] = (int32_t)p;
+    op->local_rows[p] = mine[p];
+  }
+  for (int64_t l = 0; l < nl; ++l) {
+    op->g2l[Lr[l]] = (int32_t)(ns + l);
+    op->local_rows[ns + l] = Lr[l];
+  }
+  // local CSR in local column indices, each row ascending: own short rows whole; long
+  // rows restricted to the columns this rank owns (long-row columns: rank 0). The
+  // long rows' 8 column slices then split this rank's own columns, so every XCD
+  // gets a share of the long-row work.
+  op->h_rowptr.assign(1, 0);
+  std::vector<std::pair<int32_t, double>> row;
+  for (int64_t p = 0; p < op->n; ++p) {
+    const int64_t i = op->local_rows[p];
+    const bool is_long = p >= ns;
+    row.clear();
+    for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
+      const int32_t c = col_idx[q];
+      if (is_long && !(lidx[c] < 0 ? owner[c] == me : me == 0)) continue;
+      row.emplace_back(op->g2l[c], vals[q]);
+    }
+    std::sort(row.begin(), row.end(),
+              [](const std::pair<int32_t, double>& a, const std::pair<int32_t, double>& b) {
+                return a.first < b.first;
+              });
+    for (const auto& e : row) {
+      op->h_col.push_back(e.first);
+      op->h_val.push_back(e.second);
+    }
+    op->h_rowptr.push_back((int32_t)op->h_col.size());
+  }
+  op->nnz = (int64_t)op->h_col.size();
+  op->sp.long_from = ns;
+  op->nch.resize(R);
+  for (int r = 0; r < R; ++r)
+    op->nch[r] = (int32_t)((cut[r + 1] - cut[r] + kChunkRows - 1) / kChunkRows);
 }
 
 } // namespace
@@ -998,6 +1129,10 @@ tpl_status tpl_op_create_csr(tpl_ctx_t ctx, int64_t n, int64_t nnz, const int64_
 tpl_status tpl_op_destroy(tpl_op_t op) {
   return guarded([&] {
     if (!op) return;
+    if (op->plan_only) {  // host vectors only
+      delete op;
+      return;
+    }
     hipSetDevice(op->device);
     hipStreamSynchronize(op->stream);
     drop_graphs(op);
@@ -1016,7 +1151,7 @@ int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
   return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0) |
          (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0) | (op->last_one_graph ? 32 : 0) |
-         (op->d_perm || op->local_order ? 64 : 0);
+         (!op->perm.empty() || op->local_order ? 64 : 0);
 }
 
 tpl_status tpl_op_set_reorder(tpl_op_t op, int mode) {
@@ -1678,7 +1813,7 @@ tpl_status tpl_op_set_order_groups(tpl_op_t op, int32_t groups) {
 
 int32_t tpl_op_order_groups(tpl_op_t op) {
   if (!op) return -1;
-  return op->d_perm ? op->sp.order_groups : 0;
+  return !op->perm.empty() ? op->sp.order_groups : 0;
 }
 
 // ------------------------------------------------------------ row partition
@@ -1793,112 +1928,14 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
                                          tpl_op_t* out) {
   return guarded([&] {
     if (!d || !row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
-    const int R = d->nranks, me = d->rank;
-    const int64_t nnz = row_ptr[n];
-    if (n < 1 || n >= INT32_MAX / 2 || nnz >= INT32_MAX || row_ptr[0] != 0)
-      fail(TPL_ERR_INVALID_ARGUMENT, "bad CSR sizes");
-    if (nnz > 0 && !vals) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
-    check_csr(n, n, row_ptr, col_idx);
-    std::vector<int32_t> rp32(n + 1);
-    for (int64_t i = 0; i <= n; ++i) rp32[i] = (int32_t)row_ptr[i];
-    // short / long rows by the global rule; long rows are replicated on every rank
-    const int32_t T = short_row_threshold(n, rp32, -1);
-    std::vector<int64_t> S, Lr;
-    std::vector<int32_t> lidx(n, -1);
-    for (int64_t i = 0; i < n; ++i) {
-      if (rp32[i + 1] - rp32[i] > T) {
-        lidx[i] = (int32_t)Lr.size();
-        Lr.push_back(i);
-      } else {
-        S.push_back(i);
-      }
-    }
-    if ((int64_t)S.size() < R) fail(TPL_ERR_UNSUPPORTED, "fewer short rows than ranks");
-    // short rows in contiguous blocks balanced by bytes: the row itself plus the
-    // long-row entries in its column, which the owner of that column computes
-    std::vector<int32_t> longcnt(n, 0);
-    for (int64_t l : Lr)
-      for (int64_t q = row_ptr[l]; q < row_ptr[l + 1]; ++q) longcnt[col_idx[q]]++;
-    std::vector<double> prefix(S.size() + 1, 0.0);
-    for (size_t p = 0; p < S.size(); ++p) {
-      const int64_t i = S[p];
-      prefix[p + 1] = prefix[p] + 12.0 * (double)(rp32[i + 1] - rp32[i] + longcnt[i]) + 40.0;
-    }
-    std::vector<int64_t> cut(R + 1);
-    balanced_cuts(prefix, R, cut.data());
-    std::vector<int32_t> owner(n, -1);
-    for (int r = 0; r < R; ++r)
-      for (int64_t p = cut[r]; p < cut[r + 1]; ++p) owner[S[p]] = r;
-    // halo-free check (all ranks decide alike: they all see the whole matrix)
-    for (int64_t i : S)
-      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
-        const int32_t c = col_idx[q];
-        if (lidx[c] < 0 && owner[c] != owner[i])
-          fail(TPL_ERR_UNSUPPORTED, "a short row references a short row of another rank "
-                                    "(use the row-partitioned operator)");
-      }
     HIPCHK(hipSetDevice(d->ctx.device));
     auto op = std::make_unique<tpl_op_s>();
     op->ctx = &d->ctx;
     op->device = d->ctx.device;
     op->stream = d->ctx.stream;
     op->dist = d;
-    op->hybrid = true;
     op->eager = d->comm == nullptr;
-    op->n_glob = n;
-    const int64_t ns = cut[me + 1] - cut[me], nl = (int64_t)Lr.size();
-    op->ns_local = ns;
-    op->n = ns + nl;
-    // this rank's short rows; in the locality order (tpl_layout.h locality_order, the
-    // same key over the replicated long rows' ranks) when the rank's rows fit the auto
-    // rule. The local order is the caller's to follow through tpl_op_local_rows, so no
-    // vector is permuted on the device.
-    std::vector<int64_t> mine(S.begin() + cut[me], S.begin() + cut[me + 1]);
-    if (nl > 0 && op->n <= kReorderAutoMaxRows) {
-      // lidx is each long row's rank among the long rows, as locality_order ranks them
-      locality_sort(mine, row_ptr, col_idx, lidx.data(), (int32_t)nl, op->sp.order_groups);
-      op->local_order = true;
-    }
-    op->g2l.assign(n, -1);
-    op->local_rows.resize(op->n);
-    for (int64_t p = 0; p < ns; ++p) {
-      op->g2l[mine[p]] = (int32_t)p;
-      op->local_rows[p] = mine[p];
-    }
-    for (int64_t l = 0; l < nl; ++l) {
-      op->g2l[Lr[l]] = (int32_t)(ns + l);
-      op->local_rows[ns + l] = Lr[l];
-    }
-    // local CSR in local column indices, each row ascending: own short rows whole; long
-    // rows restricted to the columns this rank owns (long-row columns: rank 0). The
-    // long rows' 8 column slices then split this rank's own columns, so every XCD
-    // gets a share of the long-row work.
-    op->h_rowptr.assign(1, 0);
-    std::vector<std::pair<int32_t, double>> row;
-    for (int64_t p = 0; p < op->n; ++p) {
-      const int64_t i = op->local_rows[p];
-      const bool is_long = p >= ns;
-      row.clear();
-      for (int64_t q = row_ptr[i]; q < row_ptr[i + 1]; ++q) {
-        const int32_t c = col_idx[q];
-        if (is_long && !(lidx[c] < 0 ? owner[c] == me : me == 0)) continue;
-        row.emplace_back(op->g2l[c], vals[q]);
-      }
-      std::sort(row.begin(), row.end(),
-                [](const std::pair<int32_t, double>& a, const std::pair<int32_t, double>& b) {
-                  return a.first < b.first;
-                });
-      for (const auto& e : row) {
-        op->h_col.push_back(e.first);
-        op->h_val.push_back(e.second);
-      }
-      op->h_rowptr.push_back((int32_t)op->h_col.size());
-    }
-    op->nnz = (int64_t)op->h_col.size();
-    op->sp.long_from = ns;
-    op->nch.resize(R);
-    for (int r = 0; r < R; ++r)
-      op->nch[r] = (int32_t)((cut[r + 1] - cut[r] + kChunkRows - 1) / kChunkRows);
+    fill_replicated(op.get(), d->nranks, d->rank, n, row_ptr, col_idx, vals);
     init_op(op.get());
     *out = op.release();
   });
@@ -1913,6 +1950,65 @@ tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows) {
       const int64_t r0 = op->dist ? op->starts[op->dist->rank] : 0;
       for (int64_t i = 0; i < op->n; ++i) rows[i] = r0 + i;
     }
+  });
+}
+
+// ------------------------------------------------------------ host-only plans
+tpl_status tpl_plan_create(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
+                           const double* vals, int mode, int nranks, int rank,
+                           int32_t order_groups, tpl_op_t* out) {
+  return guarded([&] {
+    if (!row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (mode < TPL_PLAN_SINGLE || mode > TPL_PLAN_ROWS)
+      fail(TPL_ERR_INVALID_ARGUMENT, "plan mode must be TPL_PLAN_SINGLE, _REPLICATED or _ROWS");
+    if (mode == TPL_PLAN_SINGLE ? (nranks != 1 || rank != 0)
+                                : (nranks < 1 || rank < 0 || rank >= nranks))
+      fail(TPL_ERR_INVALID_ARGUMENT, "bad rank / nranks");
+    if (order_groups < 0) fail(TPL_ERR_INVALID_ARGUMENT, "group count must be >= 0 (0: default 16)");
+    if (n < 0) fail(TPL_ERR_INVALID_ARGUMENT, "negative size");
+    const int64_t nnz = row_ptr[n];
+    if (nnz > 0 && (!vals || !col_idx)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+    auto op = std::make_unique<tpl_op_s>();
+    op->plan_only = true;
+    if (mode == TPL_PLAN_SINGLE) {  // tpl_op_create_csr's host half
+      if (n >= INT32_MAX || nnz >= INT32_MAX)
+        fail(TPL_ERR_UNSUPPORTED, "n and nnz must be < 2^31 (int32 device offsets)");
+      check_csr(n, n, row_ptr, col_idx);
+      op->n = op->n_glob = n;
+      op->nnz = nnz;
+      op->h_rowptr.assign(row_ptr, row_ptr + n + 1);
+      op->h_col.assign(col_idx, col_idx + nnz);
+      op->h_val.assign(vals, vals + nnz);
+      if (order_groups > 0) op->sp.order_groups = order_groups;
+    } else {
+      op->plan_dist = std::make_unique<tpl_dist_s>();
+      op->plan_dist->rank = rank;
+      op->plan_dist->nranks = nranks;
+      op->dist = op->plan_dist.get();
+      if (mode == TPL_PLAN_REPLICATED) {
+        fill_replicated(op.get(), nranks, rank, n, row_ptr, col_idx, vals);
+      } else {  // the block tpl_dist_partition gives this rank (tpl_dist_op_create_csr)
+        if (n < nranks) fail(TPL_ERR_INVALID_ARGUMENT, "fewer rows than ranks");
+        if (n >= INT32_MAX / 2) fail(TPL_ERR_UNSUPPORTED, "n must be < 2^30");
+        check_csr(n, n, row_ptr, col_idx);
+        std::vector<double> prefix(n + 1);
+        for (int64_t i = 0; i <= n; ++i) prefix[i] = 12.0 * (double)row_ptr[i] + 40.0 * (double)i;
+        op->starts.resize(nranks + 1);
+        balanced_cuts(prefix, nranks, op->starts.data());
+        const int64_t r0 = op->starts[rank], r1 = op->starts[rank + 1];
+        op->n = r1 - r0;
+        op->n_glob = n;
+        op->nnz = row_ptr[r1] - row_ptr[r0];
+        if (op->nnz >= INT32_MAX) fail(TPL_ERR_UNSUPPORTED, "nnz must be < 2^31");
+        op->h_rowptr.resize(op->n + 1);
+        for (int64_t i = 0; i <= op->n; ++i) op->h_rowptr[i] = (int32_t)(row_ptr[r0 + i] - row_ptr[r0]);
+        op->h_col.assign(col_idx + row_ptr[r0], col_idx + row_ptr[r1]);
+        op->h_val.assign(vals + row_ptr[r0], vals + row_ptr[r1]);
+      }
+    }
+    set_stride(op.get());
+    rebuild_schedule(op.get());  // the layout only (plan_only: nothing is uploaded)
+    *out = op.release();
   });
 }
 

@@ -74,6 +74,54 @@ def _is_torch_cuda(x) -> bool:
     return type(x).__module__.startswith("torch") and getattr(x, "is_cuda", False)
 
 
+class HostPlan:
+    """The host half of an operator (tpl_plan_create): rows, order and SpMV layout of a
+    single-GPU operator (``mode="single"``, ``order_groups`` as set_order_groups) or of
+    rank ``rank`` of a partition (``"replicated"`` / ``"rows"``), computed by the
+    runtime's own code with no GPU. ``schedule()`` and ``local_rows`` are what the live
+    operator would report; every device call on it fails."""
+
+    _MODES = {"single": 0, "replicated": 1, "rows": 2}
+
+    def __init__(self, a, mode: str = "single", nranks: int = 1, rank: int = 0,
+                 order_groups: int = 0):
+        n, rp, ci, v = _as_csr_arrays(a)
+        h = c_void_p()
+        check(_lib.tpl_plan_create(n, rp.ctypes.data_as(POINTER(c_int64)),
+                                   ci.ctypes.data_as(POINTER(c_int32)),
+                                   v.ctypes.data_as(POINTER(c_double)), self._MODES[mode],
+                                   int(nranks), int(rank), int(order_groups), byref(h)))
+        self._op = h.value
+        self.mode = mode
+        self._n = int(_lib.tpl_op_nrows(self._op))
+        rows = np.zeros(max(self._n, 1), dtype=np.int64)
+        check(_lib.tpl_op_local_rows(self._op, rows.ctypes.data_as(POINTER(c_int64))))
+        self.local_rows = rows[:self._n]
+
+    schedule = None  # bound below (HipCsrOp.schedule: host reads only)
+
+    @property
+    def handle(self) -> int:
+        return self._op
+
+    def flags(self) -> int:
+        return int(_lib.tpl_op_flags(self._op))
+
+    def order_groups(self) -> int:
+        return int(_lib.tpl_op_order_groups(self._op))
+
+    def close(self):
+        if getattr(self, "_op", None):
+            _lib.tpl_op_destroy(self._op)
+            self._op = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class HipCsrOp:
     """Symmetric sparse operator resident in the HBM of one MI355X.
 
@@ -256,3 +304,6 @@ class HipCsrOp:
 
     def __repr__(self):
         return f"HipCsrOp(n={self._n}, nnz={self._nnz}, device={self.device})"
+
+
+HostPlan.schedule = HipCsrOp.schedule
