@@ -65,3 +65,21 @@ for name, vals in blocks.items():
 with open(os.path.join(prof, "pmc_pass_one.json"), "w") as f:
     json.dump(p1, f, indent=1)
 print(p1)
+# in-graph average duration of both SpMV kernels of the headline (rocprofv3 --stats of
+# the --headline-only run): bench.py reads it for roofline.spmv_kernels_rocprof
+stats = {}
+import csv
+with open(os.path.join(out, "prof", "run_kernel_stats.csv")) as f:
+    for r in csv.DictReader(f):
+        m = re.search(r"tpl::(k_p[12]_spmv|k_p1_axpy)(<\d+>)", r["Name"])
+        if m and m.group(1) + m.group(2) in ("k_p1_spmv<58>", "k_p2_spmv<58>", "k_p1_axpy<12>"):
+            stats[m.group(1)] = {"avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"]),
+                                 "percentage": float(r["Percentage"])}
+rj = {"config": CFG, "avg_ns": {k: v["avg_ns"] for k, v in stats.items()},
+      "calls": {k: v["calls"] for k, v in stats.items()},
+      "percentage_of_gpu_time": {k: v["percentage"] for k, v in stats.items()},
+      "source": f"profiles/{tag}_kernel_stats.csv (rocprofv3 --kernel-trace --stats, bench.py "
+                "--headline-only 1 --steps 5 --warmup 1)"}
+with open(os.path.join(prof, "rocprof_headline.json"), "w") as f:
+    json.dump(rj, f, indent=1)
+print(rj)

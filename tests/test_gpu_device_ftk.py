@@ -194,3 +194,45 @@ def test_one_pass_device_f(kkt5k):
     xd = solvers.lanczos(opd, np.ones(150), 20, ftk.INV)
     assert opd.flags() & ONE_GRAPH
     assert np.linalg.norm(xd - 1.0 / np.repeat([1.0, 2.0, 3.0], 50)) < 1e-12
+
+
+def test_device_inv_headline_k500(kkt_tmp):
+    """The headline workload (500k arcs, pinned order, k = 500) with the device inv forced:
+    T_k's LU eliminated during pass one (k_p1_axpy's extra workgroup) and the back
+    substitution with Markstein divisions — x bit for bit the host-f solve's, which the
+    parity fixture pins (tests/golden/parity.json `headline`)."""
+    import hashlib
+    import json
+    import os
+    from conftest import load_kkt, ROOT
+    a = load_kkt(500000, kkt_tmp).a
+    b = harness_b(a)
+    op = HipCsrOp(a)
+    op.set_order_groups(13)
+    xd, xh = both_paths(op, b, 500)
+    assert same_bits(xd, xh)
+    with open(os.path.join(ROOT, "tests", "golden", "parity.json")) as f:
+        assert hashlib.sha256(xd.tobytes()).hexdigest()[:16] == json.load(f)["workloads"]["headline"]["x"]
+    op.close()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_device_inv_kernel_any_tridiagonal(kkt5k, seed):
+    """k_ftk_inv alone (tpl_op_ftk_device: every elimination row on the device, then the
+    back substitution) against the host solver on random T_k of 1..1365 rows: ordinary
+    scales, 1e-300 / 1e300 scales (div_rn's range check hands those rows to IEEE
+    division), exact zeros on the diagonal (pivoting, singular T_k: non-finite y' at the
+    same positions) — y' bit for bit."""
+    rng = np.random.default_rng(seed)
+    op = HipCsrOp(kkt5k.a)
+    for n in (1, 2, 3, 7, 64, 500, 1365):
+        for scale in (1.0, 1e-300, 1e300, 1e-160):
+            al = rng.standard_normal(n) * scale
+            be = rng.standard_normal(max(n - 1, 0)) * scale
+            if seed % 2:
+                al[rng.random(n) < 0.5] = 0.0  # zero diagonal entries: row swaps, zeros in x
+            yd, on = op.ftk_device("inv", al, be)
+            assert on
+            yh = ftk.INV(al, be)
+            assert same_bits_nan(yd, yh), (n, scale)
+    op.close()

@@ -69,3 +69,18 @@ def test_cpp_api_gpu(drivers):
     property tests on the 5k KKT instance (TOLERANCE 5e-9), and the solver-closure errors."""
     dmx, qfc, _ = drivers
     _run([os.path.join(NATIVE, "build", "cpp_api_test"), "--gpu", dmx, qfc])
+
+
+def test_back_substitution_division_is_ieee(tmp_path):
+    """k_ftk_inv's back substitution divides with Markstein's correction from a
+    precomputed reciprocal (tpl_kernels.hip div_rn); restated on the host with the same
+    fused multiply-adds, it gives the IEEE quotient bit for bit on every pair its range
+    check lets through (2e7 pairs: wide exponents, near-exact and binade-boundary
+    quotients, signed zeros)."""
+    cc = os.environ.get("CC", "gcc")
+    if shutil.which(cc) is None:
+        pytest.skip("no host C compiler")
+    exe = str(tmp_path / "div_rn_check")
+    subprocess.run([cc, "-O2", "-mfma", "-ffp-contract=off", "-o", exe,
+                    os.path.join(NATIVE, "div_rn_check.c"), "-lm"], check=True)
+    _run([exe, "20000000"])

@@ -177,12 +177,16 @@ struct CsrDev {
 constexpr int kFlagBytes = 32;       // DevState::flags: 8 int32
 struct DevState {
   int32_t* flags;   // [0] stop, [1] error (1 = zero b), [2] steps_taken, [3] second
-                    // Gram-Schmidt passes, [4] device f(T_k) handed back to the host
+                    // Gram-Schmidt passes, [4] device f(T_k) handed back to the host,
+                    // [5] rows of T_k's LU eliminated during pass one (k_p1_axpy)
   double* norms;    // [0] = ||b||, [j] = beta_j                         (kcap+1)
   double* alphas;   // alphas[j-1] = alpha_j                              (kcap)
   double* betas;    // betas[j-1]  = beta_j                               (kcap)
   double* y;        // pass-two coefficients y_k (already * ||b||), or y' (kcap)
   double* p2c;      // pass-two step records, 8 doubles per step (k_p2_coefs, EpiPass2R)
+  double* lu;       // T_k's LU built during pass one (one-graph inv): D | DU | DU2 | B
+                    // (kcap each), then the running row (d, du, b)        (4 kcap + 3)
+  int32_t kcap;     // capacity of the k-sized arrays
   double* Pa;       // alpha partials (NA) — written by this rank's kernels
   double* Pb;       // ||.||^2 partials (G2)
   // What the reducing kernels read: Pa / Pb on one GPU; with the rows partitioned

@@ -50,6 +50,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_init(CsrDev A, DevState S,
     S.flags[2] = 0;
     S.flags[3] = 0;
     S.flags[4] = 0;
+    S.flags[5] = 0;
   }
   const int rb = elem_block(A, blockIdx.x);
   if (rb < 0) return;
@@ -188,16 +189,104 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 4)) void k_p1_spmv_wide(CsrDe
   p1_spmv_body<F, 4>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
 }
 
+// ---- T_k^{-1} e_1 on the device (the one-graph inv): the host solver's operations
+// (tpl_ftk.cpp: the LAPACK dgtsv scheme, tridiagonal elimination with partial pivoting,
+// then back substitution), bit for bit.
+// Running row i of the elimination: its pivot, super-diagonal and right-hand side.
+struct LuRow {
+  double d, du, b;
+};
+// Eliminate row i (dl = beta_i, d1 = alpha_{i+1}, du1 = beta_{i+1} or 0 when row i + 1 is
+// the last; more = row i + 2 exists): stores row i of U (D, DU, DU2) and of the
+// transformed right-hand side (B), advances `cur` to row i + 1. The operations of the
+// host loop in its order (-ffp-contract=off).
+__device__ __forceinline__ void lu_row(int i, bool more, double dli, double d1, double du1,
+                                       LuRow& cur, double* D, double* DU, double* DU2,
+                                       double* B) {
+  double dip1 = d1, duip1 = du1, bip1 = 0.0, du2i = 0.0;
+  if (fabs(cur.d) >= fabs(dli)) {
+    const double fact = dli / cur.d;
+    dip1 = dip1 - fact * cur.du;
+    bip1 = bip1 - fact * cur.b;
+    D[i] = cur.d;
+    DU[i] = cur.du;
+    B[i] = cur.b;
+  } else {
+    const double fact = cur.d / dli;
+    D[i] = dli;
+    const double temp = dip1;
+    dip1 = cur.du - fact * temp;
+    if (more) {
+      du2i = duip1;
+      duip1 = -fact * du2i;
+    }
+    DU[i] = temp;
+    B[i] = bip1;            // b[i] <- old b[i+1] (= 0: b[i+1] is first set at step i)
+    bip1 = cur.b - fact * bip1;
+  }
+  DU2[i] = du2i;
+  cur.d = dip1;
+  cur.du = duip1;
+  cur.b = bip1;
+}
+// a / b given y = RN(1 / b): Markstein's correction q = RN(q0 + RN(a - b q0) y), q0 =
+// RN(a y), is the correctly rounded quotient — the IEEE division's bits — whenever no
+// intermediate leaves the normal range; elsewhere (zeros, huge or tiny magnitudes,
+// non-finite values) the IEEE division itself. Three dependent operations instead of the
+// division's ten on the back substitution's chain. (Checked against IEEE division on
+// 10^9 random pairs in range, exact and binade-boundary quotients included: no
+// difference; tests/native/div_rn_check.c restates it on the host, tests/test_native.py)
+__device__ __forceinline__ bool exp_in_range(double v) {
+  const unsigned e = (unsigned)(__double2hiint(v) >> 20) & 0x7FFu;  // biased exponent
+  return e - (1023u - 900u) <= 1800u;  // 2^-900 <= |v| < 2^901
+}
+__device__ __forceinline__ double div_rn(double a, double b, double y, bool b_ok) {
+  if (b_ok && exp_in_range(a)) {
+    const double q0 = a * y;
+    const double q = fma(fma(-b, q0, a), y, q0);
+    if (exp_in_range(q)) return q;
+  } else if (b_ok && a == 0.0) {
+    return a * y;  // +-0 with the quotient's sign
+  }
+  return a / b;
+}
+
 // Pass one / standard, step j: alpha_j; r_{j+1} = w - alpha_j v_j; ||r_{j+1}||^2 partials.
 // NP: alpha partials loaded per thread up front (the launcher picks the smallest of 2, 4,
 // 8, 12 with 256 NP >= NA_r; more are reduced in batches): clamped duplicate loads of a
 // small partial array only cost issue slots and cache traffic.
+// elim (one-graph inv): one more workgroup (the last) eliminates row j - 3 of T_k's LU
+// (lu_row): its inputs beta_{j-3}, alpha_{j-2} and beta_{j-2} (0-based) are all known
+// once this step's k_p1_spmv has reduced beta — the row is done off the critical path,
+// so only the last rows and the back substitution remain after pass one (k_ftk_inv).
 template <int NP>
 __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   const double* __restrict__ W,
                                                   const double* __restrict__ r_cur,
-                                                  double* __restrict__ r_next, int j, int k) {
+                                                  double* __restrict__ r_next, int j, int k,
+                                                  int elim) {
   __shared__ double red[4];
+  if (elim && blockIdx.x == gridDim.x - 1) {
+    if (threadIdx.x != 0 || j < 3) return;
+    const int i = j - 3;
+    double* D = S.lu;
+    double* st = S.lu + 4 * (size_t)S.kcap;
+    // every input with the flags (one round trip): the row's coefficients and the running
+    // row (the initial one at i = 0: alpha_0, beta_0, 1)
+    const int stop = S.flags[0], done = S.flags[5];
+    const double dli = S.betas[i], d1 = S.alphas[i + 1], du1 = S.betas[i + 1];
+    LuRow cur{st[0], st[1], st[2]};
+    const double a0 = S.alphas[0];
+    if (stop || done != i) return;  // breakdown at this step: the tail finishes the rows
+    if (i == 0) cur = LuRow{a0, dli, 1.0};
+    lu_row(i, true, dli, d1, du1, cur, D, D + S.kcap, D + 2 * (size_t)S.kcap,
+           D + 3 * (size_t)S.kcap);
+    st[0] = cur.d;
+    st[1] = cur.du;
+    st[2] = cur.b;
+    S.flags[5] = i + 1;
+    return;
+  }
   // every kernel argument in one scalar round trip
   asm volatile("" ::"s"(A.E), "s"(A.n), "s"(A.norm_n), "s"(A.NA_r), "s"(S.Pa_r), "s"(S.flags),
                "s"(S.norms), "s"(S.alphas), "s"(S.Pb));
@@ -367,81 +456,99 @@ __global__ __launch_bounds__(kTPB) void k_p2_tail(int64_t n, DevState S, double*
   }
 }
 
-// f(T_k) = T_k^{-1} on the device: y = ||b|| * T_k^{-1} e_1, the same operations in the
-// same order as the host solver tpl_ftk_inv (tpl_ftk.cpp: tridiagonal elimination with
-// partial pivoting, the LAPACK dgtsv scheme, then back substitution), so the two agree
-// bit for bit (IEEE division, -ffp-contract=off). The elimination is one dependent chain:
-// the 256 threads stage alpha and beta in LDS, lane 0 runs the chain with the running row
-// (d_i, du_i, b_i) in registers and the next row's inputs read ahead from LDS, the
-// eliminated rows go to LDS, and the back substitution writes y. One-graph solve only
-// (tpl_runtime.cpp): reads steps_taken and ||b|| from the solver state; dynamic LDS:
-// 6 kcap doubles.
+// f(T_k) = T_k^{-1} on the device: y = ||b|| * T_k^{-1} e_1, bit for bit the host solver
+// tpl_ftk_inv (tpl_ftk.cpp: the LAPACK dgtsv scheme — tridiagonal elimination with partial
+// pivoting, then back substitution; IEEE operations, -ffp-contract=off). Both halves are
+// one dependent chain. The elimination's rows [0, flags[5]) were done during pass one by
+// k_p1_axpy's extra workgroup (one row per step, one-graph inv); the rest — the last
+// rows, or all of them (tpl_op_ftk_device, the one-pass solver) — run here on lane 0
+// with alpha and beta staged in LDS. The back substitution divides by pivots known before
+// it starts, so their reciprocals are taken first on all lanes and every division of the
+// chain becomes Markstein's correction (div_rn: three dependent operations, the IEEE
+// quotient's bits); a row whose operands leave div_rn's range sets a flag and the whole
+// substitution is redone with IEEE divisions. Dynamic LDS: 7 kcap doubles.
 // scale: 1 — y = ||b|| y' (two-pass: y_k, src/solvers.rs:169); 0 — y' itself (one-pass:
 // the reconstruction multiplies by ||b||, src/solvers.rs:96-104); x * 1.0 is exact.
 __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S, int scale) {
   extern __shared__ double sh[];
+  __shared__ double last[3];
   const int n = S.flags[2];
   if (S.flags[1] || n < 1) return;
-  double* al = sh;           // alpha (n)
-  double* be = sh + n;       // beta (n - 1)
-  double* D = sh + 2 * n;    // eliminated rows: d, du, du2, rhs
-  double* DU = sh + 3 * n;
-  double* DU2 = sh + 4 * n;
-  double* B = sh + 5 * n;
+  const size_t kc = (size_t)S.kcap;
+  const int done = min(S.flags[5], max(n - 1, 0));  // rows eliminated during pass one
+  double* D = sh;
+  double* DU = sh + n;
+  double* DU2 = sh + 2 * n;
+  double* B = sh + 3 * n;
+  double* R = sh + 4 * n;   // reciprocals of the pivots
+  double* al = sh + 5 * n;  // alpha, beta of the rows still to eliminate
+  double* be = sh + 6 * n;
   for (int i = threadIdx.x; i < n; i += kTPB) {
+    if (i < done) {
+      D[i] = S.lu[i];
+      DU[i] = S.lu[kc + i];
+      DU2[i] = S.lu[2 * kc + i];
+      B[i] = S.lu[3 * kc + i];
+    }
     al[i] = S.alphas[i];
     be[i] = i + 1 < n ? S.betas[i] : 0.0;
   }
   __syncthreads();
+  if (threadIdx.x == 0) {
+    LuRow cur = done == 0 ? LuRow{al[0], n > 1 ? be[0] : 0.0, 1.0}
+                          : LuRow{S.lu[4 * kc], S.lu[4 * kc + 1], S.lu[4 * kc + 2]};
+    for (int i = done; i + 1 < n; ++i)
+      lu_row(i, i + 2 < n, be[i], al[i + 1], i + 2 < n ? be[i + 1] : 0.0, cur, D, DU, DU2, B);
+    last[0] = cur.d;
+    last[1] = cur.b;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i + 1 < n; i += kTPB) R[i] = 1.0 / D[i];
+  __syncthreads();
   if (threadIdx.x != 0) return;
   const double bnorm = scale ? S.norms[0] : 1.0;
-  double di = al[0], dui = n > 1 ? be[0] : 0.0, bi = 1.0;
-  double nx_dl = n > 1 ? be[0] : 0.0, nx_d = n > 1 ? al[1] : 0.0, nx_du = n > 2 ? be[1] : 0.0;
-  for (int i = 0; i + 1 < n; ++i) {
-    const double dli = nx_dl, d1 = nx_d, du1 = nx_du;  // dl[i], d[i+1], du[i+1] (inputs)
-    if (i + 2 < n) {  // read ahead for row i + 1
-      nx_dl = be[i + 1];
-      nx_d = al[i + 2];
-      nx_du = i + 3 < n ? be[i + 2] : 0.0;
-    }
-    double dip1 = d1, duip1 = du1, bip1 = 0.0, du2i = 0.0;
-    if (fabs(di) >= fabs(dli)) {
-      const double fact = dli / di;
-      dip1 = dip1 - fact * dui;
-      bip1 = bip1 - fact * bi;
-      D[i] = di;
-      DU[i] = dui;
-      B[i] = bi;
-    } else {
-      const double fact = di / dli;
-      D[i] = dli;
-      const double temp = dip1;
-      dip1 = dui - fact * temp;
-      if (i + 2 < n) {
-        du2i = duip1;
-        duip1 = -fact * du2i;
-      }
-      DU[i] = temp;
-      B[i] = bip1;            // b[i] <- old b[i+1] (= 0: b[i+1] is first set at step i)
-      bip1 = bi - fact * bip1;
-    }
-    DU2[i] = du2i;
-    di = dip1;
-    dui = duip1;
-    bi = bip1;
-  }
-  // back substitution with U = (D, DU, DU2)
-  double x1 = bi / di;  // b[n-1] / d[n-1]
-  S.y[n - 1] = x1 * bnorm;
-  if (n > 1) {
-    double x0 = (B[n - 2] - DU[n - 2] * x1) / D[n - 2];
+  // back substitution with U = (D, DU, DU2): x_i = ((B_i - DU_i x_{i+1}) - DU2_i x_{i+2}) / D_i
+  const double xl = last[1] / last[0];  // b[n-1] / d[n-1]
+  S.y[n - 1] = xl * bnorm;
+  if (n == 1) return;
+  bool bad = false;
+  double x1 = xl, x0;
+  {
+    const double t = B[n - 2] - DU[n - 2] * x1;
+    const bool ok = exp_in_range(D[n - 2]) && exp_in_range(R[n - 2]);
+    x0 = div_rn(t, D[n - 2], R[n - 2], ok);
     S.y[n - 2] = x0 * bnorm;
-    for (int ii = n - 3; ii >= 0; --ii) {
-      const double xi = (B[ii] - DU[ii] * x0 - DU2[ii] * x1) / D[ii];
-      S.y[ii] = xi * bnorm;
-      x1 = x0;
-      x0 = xi;
+  }
+  // the fast chain: every row's operands read one row ahead; range checks off the chain
+  double b_n = 0.0, du_n = 0.0, du2_n = 0.0, d_n = 1.0, r_n = 1.0;
+  if (n >= 3) {
+    b_n = B[n - 3]; du_n = DU[n - 3]; du2_n = DU2[n - 3]; d_n = D[n - 3]; r_n = R[n - 3];
+  }
+  for (int ii = n - 3; ii >= 0; --ii) {
+    const double bi = b_n, dui = du_n, du2i = du2_n, di = d_n, ri = r_n;
+    if (ii > 0) {
+      b_n = B[ii - 1]; du_n = DU[ii - 1]; du2_n = DU2[ii - 1]; d_n = D[ii - 1]; r_n = R[ii - 1];
     }
+    const double t = bi - dui * x0 - du2i * x1;
+    const double q0 = t * ri;
+    const double qm = fma(fma(-di, q0, t), ri, q0);
+    const double xi = t == 0.0 ? q0 : qm;  // +-0: q0 carries the quotient's sign
+    bad = bad || !(exp_in_range(di) && exp_in_range(ri) && (t == 0.0 || (exp_in_range(t) &&
+                                                                         exp_in_range(qm))));
+    S.y[ii] = xi * bnorm;
+    x1 = x0;
+    x0 = xi;
+  }
+  if (!bad) return;
+  // an operand outside div_rn's range (singular or badly scaled T_k): IEEE divisions
+  x1 = xl;
+  x0 = (B[n - 2] - DU[n - 2] * x1) / D[n - 2];
+  S.y[n - 2] = x0 * bnorm;
+  for (int ii = n - 3; ii >= 0; --ii) {
+    const double xi = (B[ii] - DU[ii] * x0 - DU2[ii] * x1) / D[ii];
+    S.y[ii] = xi * bnorm;
+    x1 = x0;
+    x0 = xi;
   }
 }
 
@@ -1095,16 +1202,16 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
   return hipGetLastError();
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
-                   double* r_next, int j, int k, hipStream_t s) {
-  const dim3 g(g2_grid(A)), b(kTPB);
+                   double* r_next, int j, int k, int elim, hipStream_t s) {
+  const dim3 g(g2_grid(A) + (elim ? 1 : 0)), b(kTPB);
   if (A.NA_r <= 2 * kTPB)
-    hipLaunchKernelGGL(k_p1_axpy<2>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+    hipLaunchKernelGGL(k_p1_axpy<2>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim);
   else if (A.NA_r <= 4 * kTPB)
-    hipLaunchKernelGGL(k_p1_axpy<4>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+    hipLaunchKernelGGL(k_p1_axpy<4>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim);
   else if (A.NA_r <= 8 * kTPB)
-    hipLaunchKernelGGL(k_p1_axpy<8>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+    hipLaunchKernelGGL(k_p1_axpy<8>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim);
   else
-    hipLaunchKernelGGL(k_p1_axpy<12>, g, b, 0, s, A, S, W, r_cur, r_next, j, k);
+    hipLaunchKernelGGL(k_p1_axpy<12>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim);
   return hipGetLastError();
 }
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,
@@ -1126,7 +1233,7 @@ hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], 
   return hipGetLastError();
 }
 hipError_t ftk_inv(const DevState& S, int kcap, int scale, hipStream_t s) {
-  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)6 * kcap * sizeof(double), s, S, scale);
+  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)7 * kcap * sizeof(double), s, S, scale);
   return hipGetLastError();
 }
 hipError_t ftk_exp(const DevState& S, int kcap, int scale, hipStream_t s) {

@@ -36,8 +36,9 @@ hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s);
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
+// elim: one more workgroup eliminates row j - 3 of T_k's LU (one-graph inv)
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
-                   double* r_next, int j, int k, hipStream_t s);
+                   double* r_next, int j, int k, int elim, hipStream_t s);
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
 hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
                    const int32_t* idx, hipStream_t s);
@@ -121,11 +122,13 @@ enum GraphKind {
   kGTwoPassDev = 4,   // one-graph solve: pass one, device f(T_k), pass two
   kGDevFtk = 5,       // (timed variant) device f(T_k) + pass-two prologue
   kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
+  kGPass1Elim = 7,    // (timed variant) pass one eliminating T_k's LU as it goes
 };
 // Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
 // run ahead of the host callback.
 constexpr int kCbBatchMax = 32;
-// One-graph solves keep the device f(T_k)'s working rows in LDS (6 k doubles, at most 64 KiB).
+// One-graph solves keep the device f(T_k)'s working rows in LDS (k_ftk_inv: 7 k doubles,
+// 76 KB at this k; gfx950 has 160 KiB of LDS per workgroup).
 constexpr size_t kDevFtkMaxK = 1365;
 // Auto mode: the device solve is one dependent chain of ~2 k fp64 divisions on one lane
 // (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
@@ -394,7 +397,8 @@ void rebuild_schedule(tpl_op_s* op) {
   op->kcap = 0;
 }
 
-// state layout: [flags: 8 int32 (kFlagBytes)] [norms kcap+1] [alphas kcap] [betas kcap] [y kcap] [Pa G] [Pb G] [Pr G*kcap]
+// state layout: [flags: 8 int32 (kFlagBytes)] [norms kcap+1] [alphas kcap] [betas kcap] [y kcap]
+// [Pa NA] [Pb G2] [p2c 8 kcap] [lu 4 kcap + 3]; reorthogonalisation partials separately (d_Pr)
 void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
   if (k > op->kcap) {
     const size_t kc = std::max<size_t>(k, 16);
@@ -406,11 +410,11 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->h_state = nullptr;
     op->d_Pr = nullptr;
     const CsrDev A = csr_dev(op);
-    // [.. | Pb G2 | pad to 64 B | p2c: 8 kc step records]
+    // [.. | Pb G2 | pad to 64 B | p2c: 8 kc step records | lu: 4 kc + 3]
     const size_t head = kFlagBytes / sizeof(double) + (kc + 1) + 3 * kc +
                         (size_t)std::max(A.NA, 1) + (size_t)A.G2;
     const size_t p2c_off = (head + 7) / 8 * 8;  // in doubles from the base (64-B aligned)
-    const size_t doubles = p2c_off - kFlagBytes / sizeof(double) + 8 * kc;
+    const size_t doubles = p2c_off - kFlagBytes / sizeof(double) + 8 * kc + 4 * kc + 3;
     const size_t bytes = kFlagBytes + doubles * sizeof(double);
     dev_alloc(op, &op->d_state, bytes);
     HIPCHK(hipMemset(op->d_state, 0, bytes));
@@ -425,6 +429,8 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
     op->S.Pa = op->S.y + kc;
     op->S.Pb = op->S.Pa + std::max(A.NA, 1);
     op->S.p2c = reinterpret_cast<double*>(base) + p2c_off;
+    op->S.lu = op->S.p2c + 8 * kc;
+    op->S.kcap = (int32_t)kc;
     // hybrid: the chunks' alpha partials go straight into this rank's pass-one segment of
     // the all-gather (k_long_epi_p1 reduces every rank's after the exchange)
     if (op->hybrid)
@@ -641,8 +647,9 @@ void enqueue_p2_exchange(tpl_op_s* op, int j) {
   }
 }
 
-// Pass one, step j (k = requested steps).
-void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
+// Pass one, step j (k = requested steps). elim: also eliminate row j - 3 of T_k's LU
+// (the one-graph inv, k_p1_axpy).
+void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false) {
   const CsrDev A = csr_dev(op, true);
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
                          op->W, Vcol, j, op->stream));
@@ -651,15 +658,16 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol) {
     HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, op->dist->nranks, r_of(op, j),
                                j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol,
                                op->d_rsum + op->dist->nranks, j, op->stream));
-  HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k, op->stream));
+  HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k,
+                         elim ? 1 : 0, op->stream));
   if (op->dist && j < k) enqueue_p1_exchange_b(op, A, j);
 }
 
-void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth) {
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false) {
   enqueue_p1_prologue(op);
   for (int j = 1; j <= (int)k; ++j) {
     double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
-    enqueue_p1_step(op, j, (int)k, Vcol);
+    enqueue_p1_step(op, j, (int)k, Vcol, elim);
     if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
   }
 }
@@ -805,9 +813,10 @@ HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
 // the events between them); no host round trip between the passes.
 void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
   const size_t key = 2 * k + (size_t)f;  // one graph per (k, f)
+  const bool elim = f == kDevInv;  // T_k's LU eliminated during pass one
   if (!op->timing) {
     run_graph(op, kGTwoPassDev, key, [&] {
-      enqueue_pass1(op, k, false, false);
+      enqueue_pass1(op, k, false, false, elim);
       enqueue_ftk_dev(op, k, f);
       enqueue_pass2_dyn_steps(op, k);
       enqueue_pass2_tail(op);
@@ -815,7 +824,7 @@ void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
     return;
   }
   HIPCHK(hipEventRecord(op->tev[0], op->stream));
-  run_graph(op, kGPass1, k, [&] { enqueue_pass1(op, k, false, false); });
+  run_graph(op, elim ? kGPass1Elim : kGPass1, k, [&] { enqueue_pass1(op, k, false, false, elim); });
   HIPCHK(hipEventRecord(op->tev[1], op->stream));
   run_graph(op, kGDevFtk, key, [&] { enqueue_ftk_dev(op, k, f); });
   HIPCHK(hipEventRecord(op->tev[2], op->stream));
@@ -1659,12 +1668,12 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
                                  op->stream));
           break;
         case TPL_KERNEL_PASS1_AXPY:
-          HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
+          HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->R[2], op->R[0], 2, big, 0, op->stream));
           break;
         case TPL_KERNEL_PASS1_STEP:  // both pass-one launches, re-running step 2
           HIPCHK(launch::p1_spmv(A1, op->S, op->RG[2], op->R[2], op->b, op->W, nullptr, 2,
                                  op->stream));
-          HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->R[2], op->R[0], 2, big, op->stream));
+          HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->R[2], op->R[0], 2, big, 0, op->stream));
           break;
         case TPL_KERNEL_PASS2_SPMV:
           HIPCHK(launch::p2_spmv(A, op->S, op->V2G[(i + 2) % 3], op->V2[(i + 2) % 3],
@@ -1686,7 +1695,7 @@ tpl_status tpl_profile_kernel(tpl_op_t op, int kernel, int iters, double* avg_us
     // Valid state for repeated launches: flags clear, partials/norms of a real step.
     HIPCHK(launch::p1_init(A1, op->S, op->b, op->stream));
     HIPCHK(launch::p1_spmv(A1, op->S, op->bG, op->b, nullptr, op->W, nullptr, 1, op->stream));
-    HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->b, op->R[2], 1, big, op->stream));
+    HIPCHK(launch::p1_axpy(A1, op->S, op->W, op->b, op->R[2], 1, big, 0, op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[1], op->b, op->n * sizeof(double), hipMemcpyDeviceToDevice,
                           op->stream));
     HIPCHK(hipMemcpyAsync(op->V2[2], op->R[2], op->n * sizeof(double), hipMemcpyDeviceToDevice,
