@@ -236,3 +236,22 @@ def test_operator_input_is_copied_and_canonicalised():
     assert np.array_equal(m.indices, before[0]) and np.array_equal(m.data, before[1])
     assert n == 3 and list(rp) == [0, 2, 3, 4]
     assert list(ci) == [0, 2, 1, 0] and list(v) == [5.0, 3.0, 0.0, 3.0]
+
+
+def test_rust_shim_binds_the_header():
+    """integration/rust/hip.rs (the reference crate's src/hip.rs; no Rust toolchain here)
+    declares only symbols include/tpl.h exports, each with the header's parameter count."""
+    src = open(os.path.join(ROOT, "integration", "rust", "hip.rs")).read()
+    block = src[src.index('extern "C" {\n    fn tpl_last_error_detail'):]
+    block = block[:block.index("\n}\n")]
+    rust = {m.group(1): m.group(2) for m in
+            re.finditer(r"fn (tpl_[a-z0-9_]+)\((.*?)\)\s*->", block, flags=re.S)}
+    hdr = open(os.path.join(ROOT, "include", "tpl.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    assert len(rust) >= 10
+    for name, params in rust.items():
+        m = re.search(rf"\b{name}\s*\((.*?)\);", hdr, flags=re.S)
+        assert m, name
+        n_h = 0 if m.group(1).strip() in ("", "void") else m.group(1).count(",") + 1
+        n_r = 0 if not params.strip() else params.count(",") + 1
+        assert n_h == n_r, (name, n_h, n_r)
