@@ -208,14 +208,21 @@ def rocprof_spmv(steps: int, b_spmv: float):
     try:
         with open(path) as f:
             rj = json.load(f)
-        t1, t2 = float(rj["avg_ns"]["k_p1_spmv"]), float(rj["avg_ns"]["k_p2_spmv"])
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError):
         return None
     frac = lambda ns: round(b_spmv / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
-    tw = (2 * steps - 1) * b_spmv / ((steps * t1 + (steps - 1) * t2) * 1e-9) / 1e9 / HBM_PEAK_GBS
-    return {"k_p1_spmv": {"avg_us": round(t1 / 1000, 3), "frac": frac(t1)},
-            "k_p2_spmv": {"avg_us": round(t2 / 1000, 3), "frac": frac(t2)},
-            "all_spmv_time_weighted_frac": round(tw, 4), "source": rj.get("source")}
+    out = {"source": rj.get("source")}
+    # mean (rocprofv3 --stats) and median ("median per-kernel time")
+    for stat, key in (("mean", "avg_ns"), ("median", "median_ns")):
+        try:
+            t1, t2 = float(rj[key]["k_p1_spmv"]), float(rj[key]["k_p2_spmv"])
+        except (KeyError, TypeError, ValueError):
+            continue
+        tw = (2 * steps - 1) * b_spmv / ((steps * t1 + (steps - 1) * t2) * 1e-9) / 1e9
+        out[stat] = {"k_p1_spmv_us": round(t1 / 1000, 3), "k_p1_spmv_frac": frac(t1),
+                     "k_p2_spmv_us": round(t2 / 1000, 3), "k_p2_spmv_frac": frac(t2),
+                     "all_spmv_time_weighted_frac": round(tw / HBM_PEAK_GBS, 4)}
+    return out if len(out) > 1 else None
 
 
 # ---- N > 1: the parent process (never touches the GPU) ------------------------------

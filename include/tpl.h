@@ -196,18 +196,20 @@ int tpl_ftk_sq(const double* alphas, size_t n_alphas, const double* betas, size_
 tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                        tpl_ftk_fn f, void* f_user, double* x_out, int mem);
 /* solvers::lanczos_two_pass (src/solvers.rs:133-175): pass one (scalars only),
- * f(T_k), y = y' ||b||, pass two regenerates V_k on the fly. With f == tpl_ftk_inv on a
- * single-GPU operator the solve can run as ONE device graph: f(T_k) on the GPU with the
- * host solver's exact operations (bitwise the same y), no host round trip between the
- * passes (tpl_op_set_device_ftk). Any other f is called on the host between the passes.
+ * f(T_k), y = y' ||b||, pass two regenerates V_k on the fly. With f == tpl_ftk_inv (or
+ * tpl_ftk_exp) on a single-GPU operator the solve runs as ONE device graph: f(T_k) on the
+ * GPU (inv: the host solver's exact operations, bitwise the same y), no host round trip
+ * between the passes (tpl_op_set_device_ftk). Any other f is called on the host between
+ * the passes.
  * On an error x_out is unspecified.                                               */
 tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, size_t k,
                                 tpl_ftk_fn f, void* f_user, double* x_out, int mem);
 /* Where tpl_lanczos_two_pass evaluates the built-in f(T_k): mode 0 = host (two graphs
  * around the host call), 1 = device (the whole solve one graph), 2 = auto (default).
- *   inv: device for k <= 1365 (mode 1) / k <= 128 (auto: the single-lane device solve,
- *        a chain of ~2k divisions with the host solver's exact operations, costs no more
- *        than the host round trip it removes there); bitwise the host result.
+ *   inv: device for k <= 1365 (modes 1 and 2): the host solver's exact operations, its
+ *        elimination done during pass one and its back substitution with correctly
+ *        rounded (Markstein) divisions — bitwise the host result, never slower than the
+ *        host round trip it removes.
  *   exp: device for k <= 1800 (modes 1 and 2): a Chebyshev expansion of exp over the
  *        Sturm-bracketed spectrum, parallel over the rows of T_k, within
  *        a small multiple of eps * exp(lambda_max) of the host QL result — the accuracy

@@ -1,3 +1,5 @@
+# Needs a lab build (scripts/build_variants.sh / build_variant_src.sh with -DTPL_LAB=1): the
+# product library ignores the TPL_SLICES layout knob.
 set -u
 cd ${GRAFT_REPO_ROOT:-$(pwd)}
 V=$PWD/two-pass-lanczos_amd/variants/libtpl_s16.so

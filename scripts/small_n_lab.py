@@ -1,5 +1,6 @@
 """Dev tool (GPU): solve time, pass-one step and isolated kernel times per element-wise
-block size (TPL_ELEM_ROWS, the lab knob of tpl_runtime.cpp rebuild_schedule) at the 50k
+block size (TPL_ELEM_ROWS, the lab knob of tpl_runtime.cpp rebuild_schedule; read only by a
+-DTPL_LAB=1 build, TPL_LIB_PATH pointing at it) at the 50k
 (k = 200, f = exp: configs[1]) and 500k (k = 500, f = inv: the headline) instances.
 ELEMS (comma list, default 512,1024,2048), ARCS (default 50000,500000), REPS."""
 import json

@@ -75,7 +75,14 @@ with open(os.path.join(out, "prof", "run_kernel_stats.csv")) as f:
         if m and m.group(1) + m.group(2) in ("k_p1_spmv<58>", "k_p2_spmv<58>", "k_p1_axpy<12>"):
             stats[m.group(1)] = {"avg_ns": float(r["AverageNs"]), "calls": int(r["Calls"]),
                                  "percentage": float(r["Percentage"])}
-rj = {"config": CFG, "avg_ns": {k: v["avg_ns"] for k, v in stats.items()},
+med = {}
+mpath = os.path.join(prof, f"{tag}_kernel_medians.json")
+if os.path.exists(mpath):
+    for name, v in json.load(open(mpath)).items():
+        for k in ("k_p1_spmv<58>", "k_p2_spmv<58>", "k_p1_axpy<12>"):
+            if name == k:
+                med[k.split("<")[0]] = round(1000.0 * v["median_us"], 1)
+rj = {"config": CFG, "avg_ns": {k: v["avg_ns"] for k, v in stats.items()}, "median_ns": med,
       "calls": {k: v["calls"] for k, v in stats.items()},
       "percentage_of_gpu_time": {k: v["percentage"] for k, v in stats.items()},
       "source": f"profiles/{tag}_kernel_stats.csv (rocprofv3 --kernel-trace --stats, bench.py "

@@ -52,7 +52,10 @@ WORKLOADS = {
                                order_groups=13),
     # configs[4] on one GPU (the N = 1 point of the 1 -> N curve)
     "configs4_1gpu": dict(arcs=5000000, k=500, f="inv", solver="two_pass", order_groups=0),
-    # configs[4] partitioned (bench.py --gpus N: the replicated-long-row partition)
+    # configs[4] partitioned (bench.py --gpus N: the replicated-long-row partition; N = 1
+    # is bench.py --gpus 1 --partition 1, one RCCL rank)
+    "configs4_replicated_N1": dict(arcs=5000000, k=500, f="inv", solver="partition",
+                                   mode="replicated", nranks=1),
     "configs4_replicated_N2": dict(arcs=5000000, k=500, f="inv", solver="partition",
                                    mode="replicated", nranks=2),
     "configs4_replicated_N4": dict(arcs=5000000, k=500, f="inv", solver="partition",

@@ -100,13 +100,15 @@ def test_device_inv_breakdown_no_op_launches():
 
 
 def test_auto_mode(kkt5k):
-    """Default (auto): one graph for k <= 128, the host solver between two graphs above."""
+    """Default (auto): one graph for the built-in inv up to k = 1365 (its LDS bound; round
+    4: never slower than the host path), the host solver between two graphs above."""
     a = kkt5k.a
     op = HipCsrOp(a)
     b = std_rng_vector(a.shape[0])
-    solvers.lanczos_two_pass(op, b, 128, ftk.INV)
-    assert op.flags() & ONE_GRAPH
-    solvers.lanczos_two_pass(op, b, 129, ftk.INV)
+    for k in (128, 129, 500, 1365):
+        solvers.lanczos_two_pass(op, b, k, ftk.INV)
+        assert op.flags() & ONE_GRAPH, k
+    solvers.lanczos_two_pass(op, b, 1366, ftk.INV)
     assert not op.flags() & ONE_GRAPH
     solvers.lanczos_two_pass(op, b, 50, ftk.EXP)  # the built-in exp: on the device too
     assert op.flags() & ONE_GRAPH
@@ -185,7 +187,12 @@ def test_one_pass_device_f(kkt5k):
         # relative_solution_deviation ~ 1e-16)
         xt = solvers.lanczos_two_pass(op, b, k, ftk.EXP)
         assert np.linalg.norm(xe - xt) <= 1e-13 * np.linalg.norm(xt), k
-    solvers.lanczos(op, b, 129, ftk.INV)  # auto: inv on the host above k = 128
+    xd = solvers.lanczos(op, b, 500, ftk.INV)  # auto: the device inv up to k = 1365
+    assert op.flags() & ONE_GRAPH
+    op.set_device_ftk(False)
+    assert same_bits_nan(xd, solvers.lanczos(op, b, 500, ftk.INV))
+    op.set_device_ftk(2)
+    solvers.lanczos(op, b, 1366, ftk.INV)  # above: the host solver
     assert not op.flags() & ONE_GRAPH
     with pytest.raises(tpl_amd.LanczosError):
         solvers.lanczos(op, np.zeros_like(b), 10, ftk.INV)

@@ -123,6 +123,7 @@ enum GraphKind {
   kGDevFtk = 5,       // (timed variant) device f(T_k) + pass-two prologue
   kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
   kGPass1Elim = 7,    // (timed variant) pass one eliminating T_k's LU as it goes
+  kGStandardElim = 8, // the standard pass eliminating T_k's LU as it goes (one-pass inv)
 };
 // Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
 // run ahead of the host callback.
@@ -130,10 +131,14 @@ constexpr int kCbBatchMax = 32;
 // One-graph solves keep the device f(T_k)'s working rows in LDS (k_ftk_inv: 7 k doubles,
 // 76 KB at this k; gfx950 has 160 KiB of LDS per workgroup).
 constexpr size_t kDevFtkMaxK = 1365;
-// Auto mode: the device solve is one dependent chain of ~2 k fp64 divisions on one lane
-// (measured 13 us at k = 50, 130 us at k = 500), the host round trip it replaces costs
-// ~15-25 us (sync, host solve, upload, launch): one graph pays up to k ~ 128.
-constexpr size_t kDevFtkAutoK = 128;
+// Auto mode: the device inv at every k it holds. Its elimination runs during pass one
+// (k_p1_axpy's extra workgroup) and its back substitution with Markstein divisions, so
+// the one-graph solve is never slower than the host round trip it replaces (round 4, same
+// box, profiles/r04_ftk_timing.txt: 0.574 vs 0.583 ms at 5k arcs k = 50, 2.390 vs 2.412
+// at 50k k = 200, 9.312 vs 9.315 ms at the 500k headline k = 500; round 3, with the
+// whole elimination after pass one and IEEE divisions, the device chain alone took 130 us
+// at k = 500 and auto mode stopped at k = 128).
+constexpr size_t kDevFtkAutoK = kDevFtkMaxK;
 // The device exp (k_ftk_exp, a Chebyshev expansion: parallel over the rows of T_k) keeps
 // 4 k + 4 doubles of dynamic LDS plus 8.2 KB of static arrays: 65.8 KB at this k, which
 // gfx950's 160 KiB of LDS per workgroup holds (a 64 KiB part would need k <= 1790).
@@ -834,7 +839,9 @@ void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
   op->p2_launches = (int64_t)k - 1;
 }
 
-void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV, int reorth) {
+// elim: eliminate T_k's LU during the pass (a device inv follows: k_ftk_inv)
+void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV, int reorth,
+                  bool elim = false) {
   ensure_state(op, k, reorth);
   if (storeV) ensure_basis(op, k);
   upload_vec(op, op->b, b, mem);
@@ -842,7 +849,8 @@ void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV,
     enqueue_pass1(op, k, true, reorth); // eager: reorth launch counts vary with j
   } else {
     if (op->timing) HIPCHK(hipEventRecord(op->tev[0], op->stream));
-    run_graph(op, storeV ? kGStandard : kGPass1, k, [&] { enqueue_pass1(op, k, storeV, false); });
+    const int kind = storeV ? (elim ? kGStandardElim : kGStandard) : (elim ? kGPass1Elim : kGPass1);
+    run_graph(op, kind, k, [&] { enqueue_pass1(op, k, storeV, false, elim); });
     if (op->timing) HIPCHK(hipEventRecord(op->tev[1], op->stream));
   }
 }
@@ -1438,16 +1446,19 @@ tpl_status tpl_lanczos(tpl_op_t op, const double* b, int64_t b_len, size_t k, tp
     set_device(op);
     check_b(op, b, b_len);
     check_k(k);
-    // 1. standard pass, V_k in HBM (src/solvers.rs:61)
-    run_pass_one(op, b, k, mem, true, false);
-    // the built-in inv / exp on the device, then the reconstruction: no host round trip
-    // (the same rules as tpl_lanczos_two_pass; y' unscaled, the GEMV multiplies by ||b||)
+    // the built-in inv / exp on the device after the standard pass, then the
+    // reconstruction: no host round trip (the same rules as tpl_lanczos_two_pass; y'
+    // unscaled, the GEMV multiplies by ||b||)
     const bool is_inv = f == &tpl_ftk_inv, is_exp = f == &tpl_ftk_exp;
     const size_t kmax = !op->device_ftk ? 0
                         : is_inv ? (op->device_ftk == 1 ? kDevFtkMaxK : kDevFtkAutoK)
                         : is_exp ? kDevExpMaxK : 0;
+    const bool dev_f = (is_inv || is_exp) && !op->dist && k <= kmax;
+    // 1. standard pass, V_k in HBM (src/solvers.rs:61); a device inv's LU eliminated
+    //    during it
+    run_pass_one(op, b, k, mem, true, false, dev_f && is_inv);
     op->last_one_graph = false;
-    if ((is_inv || is_exp) && !op->dist && k <= kmax) {
+    if (dev_f) {
       enqueue_ftk_only(op, k, is_exp ? kDevExp : kDevInv, 0);
       HIPCHK(launch::gemv_recon(op->n, -1, op->S, op->d_V, op->x, op->stream));
       const HostDecomp dd = fetch_decomp(op, k);
