@@ -30,7 +30,7 @@ for kid, name in [(3, "spmv"), (2, "p2_spmv"), (0, "p1_spmv")]:
     op.profile_kernel(kid, 20)
     st = np.zeros(K * 65536, dtype=np.uint64)
     fn(st.ctypes.data, 65536)
-    G = int(np.count_nonzero(st[0::K]))
+    G = int(np.count_nonzero(st[0:K * 60000:K]))  # below kAxpyMarkBase
     nsl = G - nch
     m = st[:K * G].reshape(G, K).astype(np.float64)
     m[m == 0] = np.nan
@@ -46,3 +46,27 @@ for kid, name in [(3, "spmv"), (2, "p2_spmv"), (0, "p1_spmv")]:
             print(f"  {nm:5s} mark{k}-start {q(tt[:,k]-tt[:,0])}")
         print(f"  {nm:5s} end        {q(tt[:,5])} | dur {q(tt[:,5]-tt[:,0])}")
     # stale marks from earlier launches are possible for marks a block did not reach
+
+# pass one as it alternates (TPL_KERNEL_PASS1_STEP: k_p1_spmv then k_p1_axpy, step 2 over
+# and over): the last pair's timelines on one clock — the boundary between the two
+# kernels is the gap from k_p1_spmv's last workgroup end to k_p1_axpy's first start
+if os.environ.get("PASS1", "1") == "1":
+    op.profile_kernel(6, 20)
+    st = np.zeros(K * 65536, dtype=np.uint64)
+    fn(st.ctypes.data, 65536)
+    AX = 60000  # kAxpyMarkBase (tpl_lab.h)
+    m = st.reshape(65536, K).astype(np.float64)
+    m[m == 0] = np.nan
+    sp_rows = m[:AX]
+    sp_rows = sp_rows[np.isfinite(sp_rows[:, 0])]
+    ax = m[AX:]
+    ax = ax[np.isfinite(ax[:, 0])]
+    base = np.nanmin(sp_rows[:, 0])
+    ts, ta = (sp_rows - base) / 100.0, (ax - base) / 100.0
+    print(f"== pass-one step (k_p1_spmv {len(ts)} workgroups, then k_p1_axpy {len(ta)}); us from the SpMV's first start")
+    print(f"  spmv  start      {q(ts[:,0])}")
+    print(f"  spmv  end        {q(ts[:,5])}")
+    print(f"  axpy  start      {q(ta[:,0])}   (gap after the SpMV's last end: {np.nanmin(ta[:,0]) - np.nanmax(ts[:,5]):.2f})")
+    for k, nm in [(1, "vectors in"), (2, "alpha known"), (3, "r stored")]:
+        print(f"  axpy  mark{k}-start {q(ta[:,k]-ta[:,0])}  ({nm})")
+    print(f"  axpy  end        {q(ta[:,5])} | dur {q(ta[:,5]-ta[:,0])}")

@@ -201,3 +201,25 @@ def test_harness_ill_conditioned_exp(op_small):
         assert np.linalg.norm(xd - xh) <= 1e-11 * np.linalg.norm(xh), k
     xt = np.exp(lam) * b
     assert np.linalg.norm(xd - xt) / np.linalg.norm(xt) < 1e-6
+
+
+def test_solvers_hand_exp_back_to_the_host():
+    """Solver-level hand-back: a spectrum far too wide for the expansion
+    (diag(-1e7 .. 0)) — the device kernel hands f(T_k) back, both solvers then run the host
+    QL inside the same call, and x is bit for bit the host-path solve's (set_device_ftk(0));
+    the one-graph flag (bit 5) is clear."""
+    n = 2000
+    lam = np.linspace(-1e7, 0.0, n)
+    a = sp.diags(lam).tocsr()
+    b = std_rng_vector(n)
+    op = HipCsrOp(a)
+    for solve in (solvers.lanczos_two_pass, solvers.lanczos):
+        for k in (5, 40):
+            x2 = solve(op, b, k, ftk.EXP)
+            assert not op.flags() & ONE_GRAPH, (solve.__name__, k)
+            op.set_device_ftk(0)
+            xh = solve(op, b, k, ftk.EXP)
+            op.set_device_ftk(2)
+            assert np.array_equal(x2, xh), (solve.__name__, k)
+            assert np.all(np.isfinite(x2))
+    op.close()

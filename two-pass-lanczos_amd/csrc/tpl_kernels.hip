@@ -293,6 +293,7 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k));
   const int rb = elem_block(A, blockIdx.x);
   if (rb < 0) return;
+  TPL_MARK_AT(kAxpyMarkBase, 0);
   PartialRegs<NP> pr;
   const int na_ = A.NA_r;
   load_partials(S.Pa_r, na_, pr);
@@ -321,8 +322,10 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   for (int q = 0; q < kAxPairs; ++q) {
     keep(w0[q].x); keep(w0[q].y); keep(rc0[q].x); keep(rc0[q].y);
   }
+  TPL_MARK_AT(kAxpyMarkBase, 1);
   if (stop) return;
   const double alpha = finish_partials(S.Pa_r, na_, pr, red);
+  TPL_MARK_AT(kAxpyMarkBase, 2);
   if (rb == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
@@ -355,8 +358,10 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   for (int64_t i0 = i00 + (int64_t)kAxPairs * 2 * kTPB; i0 < end; i0 += 2 * kTPB) // E > 2048
     step(i0, *reinterpret_cast<const double2*>(W + i0),
          *reinterpret_cast<const double2*>(r_cur + i0));
+  TPL_MARK_AT(kAxpyMarkBase, 3);
   const double p = block_sum_tail(acc, red);
   if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
+  TPL_MARK_AT(kAxpyMarkBase, 5);
 }
 
 // Pass two prologue: v_1 = b * (1/||b||); x = v_1 * y_1 (src/algorithms/lanczos_two_pass.rs:248-252).

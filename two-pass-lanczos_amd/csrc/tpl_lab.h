@@ -30,9 +30,18 @@ __device__ int g_stamps_n;  // k_ftk_exp: the expansion's term count of the last
       g_stamps[kMarks * blockIdx.x + 6] = ((unsigned long long)xcc_ << 32) | hw_; \
     }                                                                        \
   } while (0)
+// marks of a kernel that runs beside an SpMV-shaped one (k_p1_axpy): its own rows of the
+// table, kAxpyMarkBase on
+constexpr int kAxpyMarkBase = 60000;
+#define TPL_MARK_AT(base, k)                                                 \
+  do {                                                                       \
+    if (threadIdx.x == 0 && (base) + blockIdx.x < 65536)                     \
+      g_stamps[kMarks * ((base) + blockIdx.x) + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
 #else
 #define TPL_MARK(k) do {} while (0)
 #define TPL_MARK_ID() do {} while (0)
+#define TPL_MARK_AT(base, k) do {} while (0)
 #endif
 
 // k_ftk_exp: record the expansion's term count (stamp build only)
