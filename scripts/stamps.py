@@ -70,3 +70,32 @@ if os.environ.get("PASS1", "1") == "1":
     for k, nm in [(1, "vectors in"), (2, "alpha known"), (3, "r stored")]:
         print(f"  axpy  mark{k}-start {q(ta[:,k]-ta[:,0])}  ({nm})")
     print(f"  axpy  end        {q(ta[:,5])} | dur {q(ta[:,5]-ta[:,0])}")
+
+    # is the tail structural? the same pair again: per-workgroup end times of two launches
+    if os.environ.get("TAIL", "1") == "1":
+        ends = []
+        for rep in range(3):
+            op.profile_kernel(6, 20)
+            st = np.zeros(K * 65536, dtype=np.uint64)
+            fn(st.ctypes.data, 65536)
+            mm = st.reshape(65536, K)[:AX].astype(np.float64)
+            G = int(np.count_nonzero(mm[:, 0]))
+            e = (mm[:G, 5] - mm[:G, 0].min()) / 100.0
+            ends.append(e)
+            hw = st.reshape(65536, K)[:G, 6]
+        nb = G - nch  # bins first in the grid (FIRST=slices)
+        print(f"== SpMV tail: {G} workgroups ({nb} bins then {nch} chunks), 3 launches")
+        for r in range(1, 3):
+            print(f"  corr(end, launch 0 vs {r}): bins {np.corrcoef(ends[0][:nb], ends[r][:nb])[0,1]:.2f}"
+                  f" chunks {np.corrcoef(ends[0][nb:], ends[r][nb:])[0,1]:.2f}")
+        avg = np.mean(ends, axis=0)
+        order = np.argsort(-avg)[:24]
+        print("  slowest (mean end over 3): idx kind xcc se cu | end0 end1 end2")
+        for g in order:
+            kind = "bin" if g < nb else "chunk"
+            v = int(hw[g])
+            print(f"   {g:5d} {kind:5s} {(v >> 32) & 15:3d} {(v >> 13) & 7:2d} {(v >> 8) & 15:2d} | "
+                  + " ".join(f"{e[g]:5.2f}" for e in ends))
+        for kind, sel in (("bin", slice(0, nb)), ("chunk", slice(nb, G))):
+            a = avg[sel]
+            print(f"  {kind}: mean end by grid index mod 8: " + " ".join(f"{a[i::8].mean():.2f}" for i in range(8)))
