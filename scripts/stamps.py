@@ -83,7 +83,11 @@ if os.environ.get("PASS1", "1") == "1":
             e = (mm[:G, 5] - mm[:G, 0].min()) / 100.0
             ends.append(e)
             hw = st.reshape(65536, K)[:G, 6]
+            raw = mm[:G] if rep == 0 else np.concatenate([raw, mm[:G]])
         nb = G - nch  # bins first in the grid (FIRST=slices)
+        os.makedirs(os.path.join(ROOT, "gpurun_out", "diag"), exist_ok=True)
+        np.savez(os.path.join(ROOT, "gpurun_out", "diag", "pass1_stamps.npz"), raw=raw.reshape(3, G, K),
+                 hw=hw, nbins=nb, nchunks=nch)
         print(f"== SpMV tail: {G} workgroups ({nb} bins then {nch} chunks), 3 launches")
         for r in range(1, 3):
             print(f"  corr(end, launch 0 vs {r}): bins {np.corrcoef(ends[0][:nb], ends[r][:nb])[0,1]:.2f}"

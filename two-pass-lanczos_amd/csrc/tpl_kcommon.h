@@ -349,7 +349,15 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
     const int p = chunk * kChunkRows + q * kTPB + t;
     live[q] = p < A.n_short;
     const int pc = clampi(p, A.n_short - 1);
-    row[q] = A.s_identity ? pc : A.srows[pc];
+    // the row-list load waited for inside its own branch: left pending into the join it
+    // would make the identity path wait for every load in flight (the DevState loads
+    // ahead of the entries included) before issuing its entries
+    int r = pc;
+    if (!A.s_identity) {
+      r = A.srows[pc];
+      asm volatile("" : "+v"(r));
+    }
+    row[q] = r;
   }
   // Issue order = arrival order: the entries first (the gathers wait on them), then
   // the row's own vector entries (needed only by the epilogue), then the gathers.
@@ -398,20 +406,26 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
   for (int q = 0; q < kRowsPerThread; ++q) pre[q] = epi.pre(row[q]);
   const Scale sc = scale_of();
   TPL_MARK(1);
-  if (!sc.ok) return false; // stopped / breakdown (uniform)
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) keep_pre(pre[q]);
+  // The products before the stop test (uniform): kept (opaque) they pin the gathers ahead
+  // of it — tested first, the compiler sinks the gathers into the branch and every
+  // workgroup waits for the stop flag's load before it issues them.
+  double sum[kRowsPerThread];
 #pragma unroll
   for (int q = 0; q < kRowsPerThread; ++q) {
-    double sum = 0.0;
+    sum[q] = 0.0;
 #pragma unroll
     for (int k = 0; k < W; ++k) {
       double prod = a[q][k] * (xv[q][k] * sc.s);
       keep(prod);
-      sum = c[q][k] >= 0 ? sum + prod : sum;
+      sum[q] = c[q][k] >= 0 ? sum[q] + prod : sum[q];
     }
-    if (live[q]) epi.apply(row[q], sum, pre[q], acc);
   }
+  if (!sc.ok) return false; // stopped / breakdown (uniform)
+#pragma unroll
+  for (int q = 0; q < kRowsPerThread; ++q)
+    if (live[q]) epi.apply(row[q], sum[q], pre[q], acc);
   TPL_MARK(2);
   return true;
 }
@@ -534,13 +548,15 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   auto pre = epi.pre(sg.row < 0 ? 0 : sg.row);
   const Scale sc = scale_of();
   TPL_MARK(1);
-  if (!sc.ok) return; // stopped / breakdown (uniform): slots untouched
   // padding slots (col = -1) are never summed (pieces cover real entries only), so the
   // product is stored unconditionally: a select here lets the compiler sink the loads
-  // of that entry into a branch and serialise them behind everything else in flight
+  // of that entry into a branch and serialise them behind everything else in flight.
+  // The same holds for the stop test (uniform): after the LDS stores, which pin the
+  // entries and gathers ahead of it.
 #pragma unroll
   for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = a[u] * (xv[u] * sc.s);
   keep_pre(pre);
+  if (!sc.ok) return; // stopped / breakdown: slots untouched
   for (int u0 = kBinBatch * kTPB; u0 < A.bin_cap; u0 += kBinBatch * kTPB) { // bins wider than one batch (rare)
     load_bin_batch<V8, C16>(A, base + u0, cbase, c, a);
 #pragma unroll

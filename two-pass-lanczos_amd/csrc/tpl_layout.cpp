@@ -176,6 +176,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   std::vector<std::vector<std::vector<std::pair<int32_t, int32_t>>>> bins(S); // (r, fill-at-start)
   std::vector<std::vector<int32_t>> fill(S);
   std::unordered_set<int64_t> lines;  // distinct 128-B lines of the open bin (bin_lines)
+  const int segs = sp.bin_segs > 0 && sp.bin_segs < kBinSegs ? sp.bin_segs : kBinSegs;
   std::vector<int64_t> plines;
   for (int s = 0; s < S && nlb > 0; ++s) {
     lines.clear();
@@ -191,7 +192,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
         over = !lines.empty() && lines.size() + plines.size() > (size_t)sp.bin_lines;
       }
       if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
-          (int)bins[s].back().size() == kBinSegs || over) {
+          (int)bins[s].back().size() == segs || over) {
         bins[s].emplace_back();
         fill[s].push_back(0);
         lines.clear();

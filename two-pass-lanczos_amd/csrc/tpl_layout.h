@@ -23,6 +23,7 @@ struct SchedParams {
                                     // 0: kElemRows)
   int bin_lines = 0;                // > 0: also close a bin once its gathers would touch
                                     // more than this many distinct 128-B lines (lab)
+  int bin_segs = 0;                 // > 0: at most this many pieces per bin (0: kBinSegs)
 };
 
 // Host copy of the SpMV layout (tpl_device.h).
