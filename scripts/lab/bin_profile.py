@@ -40,6 +40,34 @@ for s in range(S):
         cur["cols"].append(c)
 M = max(len(b) for b in bins)
 print(f"n {n}, long rows {len(lr)}, slices {S}, bins per slice {[len(b) for b in bins]}")
+# bins' gather columns for scripts/lab/bin_gather_lab.hip: per bin (block order b = 8m + s,
+# bin_cap entries; -1 padding) in the canonical position order and sorted by column inside
+# the bin (the same set of gathers, fewer distinct lines per wave-instruction)
+if os.environ.get("DUMP"):
+    nb = 8 * M
+    canon = np.full((nb, BIN_CAP), -1, dtype=np.int32)
+    for b in range(nb):
+        m, s = b >> 3, b & 7
+        if m < len(bins[s]) and bins[s][m]["cols"]:
+            c = np.concatenate(bins[s][m]["cols"]).astype(np.int32)
+            canon[b, :len(c)] = c
+    srt = np.sort(np.where(canon < 0, np.iinfo(np.int32).max, canon), axis=1)
+    srt[srt == np.iinfo(np.int32).max] = -1
+    hdr = np.array([nb, BIN_CAP, n], dtype=np.int32)
+    with open(os.environ["DUMP"], "wb") as f:
+        f.write(hdr.tobytes()); f.write(canon.tobytes()); f.write(srt.tobytes())
+    w = canon.reshape(nb, 8, 4, 64)  # (bin, u, wave, lane): position u*256 + 64*wave + lane
+    def lines_per_instr(a):
+        a = a.reshape(nb, 8, 4, 64)
+        tot = 0
+        for x in a.reshape(-1, 64):
+            x = x[x >= 0]
+            tot += len(np.unique(x >> 4))
+        return tot / (nb * 32)
+    print("distinct 128-B lines per wave-instruction: canonical %.1f, sorted %.1f"
+          % (lines_per_instr(canon), lines_per_instr(srt)))
+    sys.exit(0)
+
 npz = np.load(os.environ.get("NPZ", os.path.join(ROOT, "gpurun_out", "diag", "pass1_stamps.npz")))
 raw = npz["raw"].astype(np.float64)  # (3, G, K)
 t0 = raw[:, :, 0].min(axis=1, keepdims=True)

@@ -471,7 +471,10 @@ __global__ __launch_bounds__(kTPB) void k_p2_tail(int64_t n, DevState S, double*
 // it starts, so their reciprocals are taken first on all lanes and every division of the
 // chain becomes Markstein's correction (div_rn: three dependent operations, the IEEE
 // quotient's bits); a row whose operands leave div_rn's range sets a flag and the whole
-// substitution is redone with IEEE divisions. Dynamic LDS: 7 kcap doubles.
+// substitution is redone with IEEE divisions. The chain runs on lane 0 with nothing else
+// on it: x' goes to LDS (all lanes scale and store y after), the range tests of its
+// numerators and quotients are deferred to all lanes (round 4: 85.6 us at k = 500 with
+// them and the global stores on the chain). Dynamic LDS: 11 k doubles.
 // scale: 1 — y = ||b|| y' (two-pass: y_k, src/solvers.rs:169); 0 — y' itself (one-pass:
 // the reconstruction multiplies by ||b||, src/solvers.rs:96-104); x * 1.0 is exact.
 __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S, int scale) {
@@ -508,53 +511,84 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S, int scale) {
     last[1] = cur.b;
   }
   __syncthreads();
-  for (int i = threadIdx.x; i + 1 < n; i += kTPB) R[i] = 1.0 / D[i];
-  __syncthreads();
-  if (threadIdx.x != 0) return;
-  const double bnorm = scale ? S.norms[0] : 1.0;
-  // back substitution with U = (D, DU, DU2): x_i = ((B_i - DU_i x_{i+1}) - DU2_i x_{i+2}) / D_i
-  const double xl = last[1] / last[0];  // b[n-1] / d[n-1]
-  S.y[n - 1] = xl * bnorm;
-  if (n == 1) return;
-  bool bad = false;
-  double x1 = xl, x0;
-  {
-    const double t = B[n - 2] - DU[n - 2] * x1;
-    const bool ok = exp_in_range(D[n - 2]) && exp_in_range(R[n - 2]);
-    x0 = div_rn(t, D[n - 2], R[n - 2], ok);
-    S.y[n - 2] = x0 * bnorm;
+  // Off the chain, on all lanes: the pivots' reciprocals, each row repacked as one
+  // 32-B record {B, DU, DU2, D} (two 16-B LDS reads per row on the chain instead of four
+  // 8-B ones), and div_rn's range test of every pivot and reciprocal.
+  double* P = sh + 7 * n;  // 4 (n - 1) doubles
+  bool pbad = false;
+  for (int i = threadIdx.x; i + 1 < n; i += kTPB) {
+    const double d = D[i], r = 1.0 / d;
+    R[i] = r;
+    typedef double d2v __attribute__((ext_vector_type(2)));
+    reinterpret_cast<d2v*>(P)[2 * i] = d2v{B[i], DU[i]};
+    reinterpret_cast<d2v*>(P)[2 * i + 1] = d2v{DU2[i], d};
+    pbad = pbad || !(exp_in_range(d) && exp_in_range(r));
   }
-  // the fast chain: every row's operands read one row ahead; range checks off the chain
-  double b_n = 0.0, du_n = 0.0, du2_n = 0.0, d_n = 1.0, r_n = 1.0;
-  if (n >= 3) {
-    b_n = B[n - 3]; du_n = DU[n - 3]; du2_n = DU2[n - 3]; d_n = D[n - 3]; r_n = R[n - 3];
-  }
-  for (int ii = n - 3; ii >= 0; --ii) {
-    const double bi = b_n, dui = du_n, du2i = du2_n, di = d_n, ri = r_n;
-    if (ii > 0) {
-      b_n = B[ii - 1]; du_n = DU[ii - 1]; du2_n = DU2[ii - 1]; d_n = D[ii - 1]; r_n = R[ii - 1];
+  const bool any_pbad = __syncthreads_or(pbad);
+  double* Y = D;   // x' of every row (D is read only through P from here on)
+  double* T = DU;  // the numerator t of every row, for the deferred range test
+  if (threadIdx.x == 0) {
+    // back substitution with U = (D, DU, DU2): x_i = ((B_i - DU_i x_{i+1}) - DU2_i x_{i+2}) / D_i
+    const double xl = last[1] / last[0];  // b[n-1] / d[n-1]
+    Y[n - 1] = xl;
+    if (n >= 2) {
+      double x1 = xl, x0;
+      {
+        const double t = B[n - 2] - DU[n - 2] * x1;
+        x0 = div_rn(t, D[n - 2], R[n - 2], !any_pbad);
+        Y[n - 2] = x0;
+        T[n - 2] = 0.0;  // row n - 2 took div_rn's own checks
+      }
+      // the fast chain: Markstein's correction with every operand read one row ahead; the
+      // range tests of t and the quotient are deferred to all lanes after the loop
+      typedef double d2v __attribute__((ext_vector_type(2)));
+      const d2v* PR = reinterpret_cast<const d2v*>(P);
+      d2v p0 = {0.0, 0.0}, p1 = {0.0, 1.0};
+      double r_n = 1.0;
+      if (n >= 3) {
+        p0 = PR[2 * (n - 3)]; p1 = PR[2 * (n - 3) + 1]; r_n = R[n - 3];
+      }
+      for (int ii = n - 3; ii >= 0; --ii) {
+        const double bi = p0.x, dui = p0.y, du2i = p1.x, di = p1.y, ri = r_n;
+        if (ii > 0) {
+          p0 = PR[2 * (ii - 1)]; p1 = PR[2 * (ii - 1) + 1]; r_n = R[ii - 1];
+        }
+        const double t = bi - dui * x0 - du2i * x1;
+        const double q0 = t * ri;
+        const double qm = fma(fma(-di, q0, t), ri, q0);
+        const double xi = t == 0.0 ? q0 : qm;  // +-0: q0 carries the quotient's sign
+        Y[ii] = xi;
+        T[ii] = t;
+        x1 = x0;
+        x0 = xi;
+      }
     }
-    const double t = bi - dui * x0 - du2i * x1;
-    const double q0 = t * ri;
-    const double qm = fma(fma(-di, q0, t), ri, q0);
-    const double xi = t == 0.0 ? q0 : qm;  // +-0: q0 carries the quotient's sign
-    bad = bad || !(exp_in_range(di) && exp_in_range(ri) && (t == 0.0 || (exp_in_range(t) &&
-                                                                         exp_in_range(qm))));
-    S.y[ii] = xi * bnorm;
-    x1 = x0;
-    x0 = xi;
   }
-  if (!bad) return;
-  // an operand outside div_rn's range (singular or badly scaled T_k): IEEE divisions
-  x1 = xl;
-  x0 = (B[n - 2] - DU[n - 2] * x1) / D[n - 2];
-  S.y[n - 2] = x0 * bnorm;
-  for (int ii = n - 3; ii >= 0; --ii) {
-    const double xi = (B[ii] - DU[ii] * x0 - DU2[ii] * x1) / D[ii];
-    S.y[ii] = xi * bnorm;
-    x1 = x0;
-    x0 = xi;
+  __syncthreads();
+  // deferred: a row whose numerator or quotient left div_rn's range (t == 0 is exact)
+  bool bad = any_pbad && n >= 2;
+  for (int i = threadIdx.x; i + 2 < n; i += kTPB) {
+    const double t = T[i];
+    bad = bad || !(t == 0.0 || (exp_in_range(t) && exp_in_range(Y[i])));
   }
+  if (__syncthreads_or(bad)) {
+    // an operand outside div_rn's range (singular or badly scaled T_k): IEEE divisions
+    if (threadIdx.x == 0) {
+      const double* PD = P;
+      double x1 = Y[n - 1];
+      double x0 = (PD[4 * (n - 2)] - PD[4 * (n - 2) + 1] * x1) / PD[4 * (n - 2) + 3];
+      Y[n - 2] = x0;
+      for (int ii = n - 3; ii >= 0; --ii) {
+        const double xi = (PD[4 * ii] - PD[4 * ii + 1] * x0 - PD[4 * ii + 2] * x1) / PD[4 * ii + 3];
+        Y[ii] = xi;
+        x1 = x0;
+        x0 = xi;
+      }
+    }
+    __syncthreads();
+  }
+  const double bnorm = scale ? S.norms[0] : 1.0;
+  for (int i = threadIdx.x; i < n; i += kTPB) S.y[i] = Y[i] * bnorm;
 }
 
 // f(T_k) = exp(T_k) on the device: y = ||b|| exp(T_k) e_1 (src/bin/stability.rs:175-193
@@ -1238,7 +1272,7 @@ hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], 
   return hipGetLastError();
 }
 hipError_t ftk_inv(const DevState& S, int kcap, int scale, hipStream_t s) {
-  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)7 * kcap * sizeof(double), s, S, scale);
+  hipLaunchKernelGGL(k_ftk_inv, dim3(1), dim3(kTPB), (size_t)11 * kcap * sizeof(double), s, S, scale);
   return hipGetLastError();
 }
 hipError_t ftk_exp(const DevState& S, int kcap, int scale, hipStream_t s) {

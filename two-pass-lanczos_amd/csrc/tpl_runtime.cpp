@@ -128,8 +128,8 @@ enum GraphKind {
 // Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
 // run ahead of the host callback.
 constexpr int kCbBatchMax = 32;
-// One-graph solves keep the device f(T_k)'s working rows in LDS (k_ftk_inv: 7 k doubles,
-// 76 KB at this k; gfx950 has 160 KiB of LDS per workgroup).
+// One-graph solves keep the device f(T_k)'s working rows in LDS (k_ftk_inv: 11 k doubles,
+// 120 KB at this k; gfx950 has 160 KiB of LDS per workgroup).
 constexpr size_t kDevFtkMaxK = 1365;
 // Auto mode: the device inv at every k it holds. Its elimination runs during pass one
 // (k_p1_axpy's extra workgroup) and its back substitution with Markstein divisions, so
