@@ -318,14 +318,14 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   __builtin_amdgcn_sched_barrier(0);
   const int stop = S.flags[0];
   const double normj = S.norms[j - 1];
-#pragma unroll
-  for (int q = 0; q < kAxPairs; ++q) {
-    keep(w0[q].x); keep(w0[q].y); keep(rc0[q].x); keep(rc0[q].y);
-  }
   TPL_MARK_AT(kAxpyMarkBase, 1);
-  if (stop) return;
+  // alpha while the vectors are in flight: its wait covers the partials (issued first)
+  // only. The reduction's LDS stores and barrier keep the vector loads ahead of it, and
+  // nothing tests the (uniform) stop flag before it: a branch there would let the compiler
+  // sink the loads into it, behind the reduction.
   const double alpha = finish_partials(S.Pa_r, na_, pr, red);
   TPL_MARK_AT(kAxpyMarkBase, 2);
+  if (stop) return;
   if (rb == 0 && threadIdx.x == 0) {
     S.alphas[j - 1] = alpha;
     S.flags[2] = j;
