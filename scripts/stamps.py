@@ -64,8 +64,22 @@ if os.environ.get("PASS1", "1") == "1":
     base = np.nanmin(sp_rows[:, 0])
     ts, ta = (sp_rows - base) / 100.0, (ax - base) / 100.0
     print(f"== pass-one step (k_p1_spmv {len(ts)} workgroups, then k_p1_axpy {len(ta)}); us from the SpMV's first start")
-    print(f"  spmv  start      {q(ts[:,0])}")
-    print(f"  spmv  end        {q(ts[:,5])}")
+    nchb = 8 * ((sch["G2"] + 7) // 8) * (sch["E"] // 512)  # chunk part of the grid
+    ff = getattr(_lib.lib, "tpl_debug_first", None)
+    if ff is not None:
+        ff.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        fst = np.zeros(65536, dtype=np.uint64)
+        ff(fst.ctypes.data, 65536)
+        f0 = (fst[:len(sp_rows)].astype(np.float64) - base) / 100.0
+        print(f"  first-instruction stamp (dispatch), bins {q(f0[:len(ts) - nchb])}  chunks {q(f0[len(ts) - nchb:])}")
+        print(f"  mark0 - first: bins {q(ts[:len(ts) - nchb, 0] - f0[:len(ts) - nchb])}  chunks {q(ts[len(ts) - nchb:, 0] - f0[len(ts) - nchb:])}")
+    nbin = len(ts) - nchb
+    for nm, sel, marks in [("bin", slice(0, nbin), [1, 2, 3, 4]), ("chunk", slice(nbin, len(ts)), [1, 2])]:
+        tt = ts[sel]
+        print(f"  {nm:5s} start      {q(tt[:,0])}")
+        for k in marks:
+            print(f"  {nm:5s} mark{k}-start {q(tt[:,k]-tt[:,0])}")
+        print(f"  {nm:5s} end        {q(tt[:,5])} | dur {q(tt[:,5]-tt[:,0])}")
     print(f"  axpy  start      {q(ta[:,0])}   (gap after the SpMV's last end: {np.nanmin(ta[:,0]) - np.nanmax(ts[:,5]):.2f})")
     for k, nm in [(1, "vectors in"), (2, "alpha known"), (3, "r stored")]:
         print(f"  axpy  mark{k}-start {q(ta[:,k]-ta[:,0])}  ({nm})")

@@ -171,6 +171,7 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 1)) void k_p1_spmv(CsrDev A, 
                                                   const double* __restrict__ r_prev,
                                                   double* __restrict__ W,
                                                   double* __restrict__ Vcol, int j) {
+  TPL_MARK_FIRST();
   __shared__ double red[4], redb[4];
   extern __shared__ double lds[];
   p1_spmv_body<F, 1>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);

@@ -38,10 +38,21 @@ constexpr int kAxpyMarkBase = 60000;
     if (threadIdx.x == 0 && (base) + blockIdx.x < 65536)                     \
       g_stamps[kMarks * ((base) + blockIdx.x) + (k)] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
+// the workgroup's very first instruction (before any kernel-argument load): tells a late
+// dispatch from a late start of the marked code
+__device__ unsigned long long g_first[65536];
+#define TPL_MARK_FIRST()                                                     \
+  do {                                                                       \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+    const unsigned long long t_ = __builtin_amdgcn_s_memrealtime();          \
+    if (threadIdx.x == 0 && blockIdx.x < 65536) g_first[blockIdx.x] = t_;    \
+    __builtin_amdgcn_sched_barrier(0);                                       \
+  } while (0)
 #else
 #define TPL_MARK(k) do {} while (0)
 #define TPL_MARK_ID() do {} while (0)
 #define TPL_MARK_AT(base, k) do {} while (0)
+#define TPL_MARK_FIRST() do {} while (0)
 #endif
 
 // k_ftk_exp: record the expansion's term count (stamp build only)
@@ -60,6 +71,9 @@ constexpr int kAxpyMarkBase = 60000;
 extern "C" int tpl_debug_stamps(unsigned long long* out, int n) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps),
                                   sizeof(unsigned long long) * tpl::kMarks * n);
+}
+extern "C" int tpl_debug_first(unsigned long long* out, int n) {
+  return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_first), sizeof(unsigned long long) * n);
 }
 extern "C" int tpl_debug_exp_terms(int* out) {
   return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(tpl::g_stamps_n), sizeof(int));
