@@ -8,7 +8,7 @@ import numpy as np
 import tpl_amd
 from tpl_amd import _lib
 from tpl_amd.utils.data_loader import load_kkt_system, write_qfc_3line
-K = 7  # kMarks (tpl_kcommon.h): marks 0..5 + the HW_ID / XCC_ID slot
+K = 9  # kMarks (tpl_lab.h): marks 0..5, the HW_ID / XCC_ID slot, marks 7..8 (bins' piece sums)
 write_qfc_3line("/tmp/t.qfc", 500000)
 a = load_kkt_system(os.path.join(ROOT, "tests/golden/kkt/netgen-500000-3.dmx.xz"), "/tmp/t.qfc").a
 n = a.shape[0]
@@ -74,7 +74,7 @@ if os.environ.get("PASS1", "1") == "1":
         print(f"  first-instruction stamp (dispatch), bins {q(f0[:len(ts) - nchb])}  chunks {q(f0[len(ts) - nchb:])}")
         print(f"  mark0 - first: bins {q(ts[:len(ts) - nchb, 0] - f0[:len(ts) - nchb])}  chunks {q(ts[len(ts) - nchb:, 0] - f0[len(ts) - nchb:])}")
     nbin = len(ts) - nchb
-    for nm, sel, marks in [("bin", slice(0, nbin), [1, 2, 3, 4]), ("chunk", slice(nbin, len(ts)), [1, 2])]:
+    for nm, sel, marks in [("bin", slice(0, nbin), [1, 2, 7, 8, 3, 4]), ("chunk", slice(nbin, len(ts)), [1, 2])]:
         tt = ts[sel]
         print(f"  {nm:5s} start      {q(tt[:,0])}")
         for k in marks:

@@ -595,6 +595,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
       if (g16 == 0 && valid) psum[j] = acc;
     }
   }
+  TPL_MARK(7);
   // The other pieces, 32 per pass: the 8-lane group t >> 3 takes one; its lane g sums
   // the piece's entries g + 8q, then a butterfly over the 8 lanes.
   const int g8 = t & 7;
@@ -616,6 +617,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
     acc = group8_sum(acc);
     if (g8 == 0 && valid) psum[j] = acc;
   }
+  TPL_MARK(8);
   __syncthreads();
   TPL_MARK(3);
   if (sg.ri < 0) return; // no piece for this thread

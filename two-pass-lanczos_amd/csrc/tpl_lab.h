@@ -13,7 +13,7 @@ namespace tpl {
 // recent SpMV-shaped launch — [0] start, [1] scale known, [2] products staged /
 // row sums done, [3] piece sums staged, [4] publish drained, [5] end — read back
 // by tpl_debug_stamps().
-constexpr int kMarks = 7;  // marks 0..5 + the workgroup's HW_ID / XCC_ID in slot 6
+constexpr int kMarks = 9;  // marks 0..5, the workgroup's HW_ID / XCC_ID in slot 6, marks 7..8
 __device__ unsigned long long g_stamps[kMarks * 65536];
 __device__ int g_stamps_n;  // k_ftk_exp: the expansion's term count of the last launch
 #define TPL_MARK(k)                                                          \
