@@ -555,7 +555,6 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   // entries and gathers ahead of it.
 #pragma unroll
   for (int u = 0; u < kBinBatch; ++u) lds[u * kTPB + t] = a[u] * (xv[u] * sc.s);
-  keep_pre(pre);
   if (!sc.ok) return; // stopped / breakdown: slots untouched
   for (int u0 = kBinBatch * kTPB; u0 < A.bin_cap; u0 += kBinBatch * kTPB) { // bins wider than one batch (rare)
     load_bin_batch<V8, C16>(A, base + u0, cbase, c, a);
@@ -583,13 +582,26 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
       const int st = starts[jc], nx = starts[jc + 1];
       const int b0 = valid ? st : 0;
       const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
+      // this lane's entries k + 16q, q ascending: whole blocks of 8 first (8 reads in
+      // flight, then 8 adds with no bounds test on the chain: the longest pieces run
+      // tens of blocks), then the last 0..7 with the tests
+      int k = b0 + g16;
+      const int cnt = k < en ? (en - k + 15) >> 4 : 0;
       double acc = 0.0;
-      for (int k0 = b0 + g16; k0 < en; k0 += 128) {  // 8 reads in flight, then the adds
+      for (int blk = cnt >> 3; blk > 0; --blk, k += 128) {
         double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 16 * u < en ? k0 + 16 * u : k0];
+        for (int u = 0; u < 8; ++u) v[u] = lds[k + 16 * u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = k0 + 16 * u < en ? acc + v[u] : acc;
+        for (int u = 0; u < 8; ++u) acc = acc + v[u];
+      }
+      const int rem = cnt & 7;
+      if (rem > 0) {
+        double v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = lds[u < rem ? k + 16 * u : k];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = u < rem ? acc + v[u] : acc;
       }
       acc = group16_sum(acc);
       if (g16 == 0 && valid) psum[j] = acc;
@@ -620,6 +632,10 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   TPL_MARK(8);
   __syncthreads();
   TPL_MARK(3);
+  // the finalising thread's row entries, loaded with the gathers, waited on only now: the
+  // piece sums' LDS stores and barriers keep their loads ahead, and the sums run while
+  // they are in flight
+  keep_pre(pre);
   if (sg.ri < 0) return; // no piece for this thread
   const double p = psum[t];
   const int ns = A.n_slices;
