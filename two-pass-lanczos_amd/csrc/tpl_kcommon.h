@@ -419,7 +419,7 @@ __device__ __forceinline__ bool short_chunk_w(const CsrDev& A, int chunk, int ba
     for (int k = 0; k < W; ++k) {
       double prod = a[q][k] * (xv[q][k] * sc.s);
       keep(prod);
-      sum[q] = c[q][k] >= 0 ? sum[q] + prod : sum[q];
+      sum[q] = sum[q] + (c[q][k] >= 0 ? prod : -0.0);  // padding adds -0.0: exact
     }
   }
   if (!sc.ok) return false; // stopped / breakdown (uniform)
@@ -465,7 +465,7 @@ __device__ __forceinline__ bool short_chunk_any(const CsrDev& A, int chunk, int 
       for (int u = 0; u < 8; ++u) {
         double prod = a[u] * (xv[u] * sc.s);
         keep(prod);
-        s = (c[u] >= 0 && k0 + u < W) ? s + prod : s;
+        s = s + ((c[u] >= 0 && k0 + u < W) ? prod : -0.0);  // padding adds -0.0: exact
       }
     }
     keep_pre(pre);
@@ -569,6 +569,9 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   starts[t] = sg.ri < 0 ? -1 - sg.start : sg.start;  // < 0: no piece (value encodes the fill)
   __syncthreads();
   TPL_MARK(2);
+  // Entries past a piece's end add -0.0 instead of being skipped by a select after the
+  // add: x + (-0.0) is x bit for bit for every x (signed zeros, infinities and NaNs
+  // included), so the sums are unchanged and the select leaves the dependent add chain.
   // Piece sums (canonical long-row order). A piece longer than kBigPiece is summed by a
   // 16-lane group — lane g sums its entries g + 16q, then the 16-lane butterfly — 16
   // such pieces per pass (every piece of a bin at once at 500k arcs, where all pieces
@@ -601,7 +604,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
 #pragma unroll
         for (int u = 0; u < 8; ++u) v[u] = lds[u < rem ? k + 16 * u : k];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = u < rem ? acc + v[u] : acc;
+        for (int u = 0; u < 8; ++u) acc = acc + (u < rem ? v[u] : -0.0);
       }
       acc = group16_sum(acc);
       if (g16 == 0 && valid) psum[j] = acc;
@@ -624,7 +627,7 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
 #pragma unroll
       for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) acc = k0 + 8 * u < en ? acc + v[u] : acc;
+      for (int u = 0; u < 8; ++u) acc = acc + (k0 + 8 * u < en ? v[u] : -0.0);
     }
     acc = group8_sum(acc);
     if (g8 == 0 && valid) psum[j] = acc;
