@@ -27,7 +27,7 @@ from oracle.rng import std_rng_vector  # noqa: E402
 al2, be2, *_ = oracle.Operator(d).pass_one(std_rng_vector(10000), 200)
 cases["diag_ill_k200"] = (al2, be2)
 op = tpl_amd.HipCsrOp(sp.diags(np.arange(1.0, 65.0)).tocsr())
-buf = (ctypes.c_ulonglong * 7)()
+buf = (ctypes.c_ulonglong * 9)()  # kMarks (tpl_lab.h)
 nterm = ctypes.c_int()
 for name, (x, y) in cases.items():
     for rep in range(3):

@@ -782,6 +782,74 @@ __global__ __launch_bounds__(kTPB) void k_ftk_exp(DevState S, int scale) {
   double Ip1 = 0.0, Im = 1.0, Ssum = 0.0;  // I_{m+1}, I_m (Miller seed), 2 sum_{m'>=m} I_m'
   double* cur = buf0;
   double* nxt = buf1;
+  if (n <= 4 * 64) {
+    // T_k of at most 256 rows (configs[1]: k = 200): ONE wave runs the recurrence, four
+    // consecutive rows per lane, the neighbour rows across lanes by DPP wave shifts — no
+    // LDS exchange and no barrier per term. The same operations on the same operands as
+    // the general loop below, row by row (zero neighbours at both ends), so the same bits.
+    if (t < 64) {
+      double f1[4], f2[4], fd[4], fl[4], fr[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * t + j;
+        const bool ok = i < n;
+        fd[j] = ok ? al[i] - c : 0.0;
+        fl[j] = (ok && i > 0) ? S.betas[i - 1] : 0.0;
+        fr[j] = (ok && i + 1 < n) ? S.betas[i] : 0.0;
+        f1[j] = f2[j] = 0.0;
+      }
+      for (int m = N; m >= 1; --m) {
+        const double left = dpp_f64<0x138>(f1[3]);   // wave_shr:1 -> row 4t - 1 (0 at lane 0)
+        const double right = dpp_f64<0x130>(f1[0]);  // wave_shl:1 -> row 4t + 4 (0 at lane 63)
+        const double am = 2.0 * Im;
+        double nv[4];
+        nv[0] = ((fl[0] * left + fd[0] * f1[0]) + fr[0] * f1[1]) * inv_r;
+        nv[1] = ((fl[1] * f1[0] + fd[1] * f1[1]) + fr[1] * f1[2]) * inv_r;
+        nv[2] = ((fl[2] * f1[1] + fd[2] * f1[2]) + fr[2] * f1[3]) * inv_r;
+        nv[3] = ((fl[3] * f1[2] + fd[3] * f1[3]) + fr[3] * right) * inv_r;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          double v = 2.0 * nv[j] - f2[j];
+          if (t == 0 && j == 0) v = v + am;
+          f2[j] = f1[j];
+          f1[j] = v;
+        }
+        Ssum = Ssum + am;
+        const double Inext = Ip1 + (2.0 * (double)m * inv_r) * Im;
+        Ip1 = Im;
+        Im = Inext;
+        if (fabs(Im) > 1e200) {
+          Im *= 1e-200; Ip1 *= 1e-200; Ssum *= 1e-200;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) { f1[j] *= 1e-200; f2[j] *= 1e-200; }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int i = 4 * t + j;
+        if (i < n) {
+          cur[i + 1] = f1[j];
+          nxt[i + 1] = f2[j];
+        }
+      }
+      if (t == 0) {
+        red[1][0] = Im;
+        red[1][1] = Ssum;
+      }
+    }
+    __syncthreads();
+    Im = red[1][0];
+    Ssum = red[1][1];
+#pragma unroll
+    for (int u = 0; u < kExpRows; ++u) {
+      const int i = t + u * kTPB;
+      if (u < R && i < n) {
+        b1[u] = cur[i + 1];
+        b2v[u] = nxt[i + 1];
+      }
+    }
+    __syncthreads();  // every lane has its rows before the tail rewrites cur
+  } else
   for (int m = N; m >= 1; --m) {
     // publish b_{m+1}, then every row forms b_m from its neighbours
 #pragma unroll
