@@ -75,3 +75,64 @@ def test_dist_protocol_two_ranks(kkt_tmp):
     b = harness_b(a)
     xo = oracle.Operator(a).lanczos_two_pass(b, 50, ftk_ref.inv)
     assert np.linalg.norm(x - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
+def _plan_worker(rank, world, port, tmp, arcs, mode):
+    """One rank of a gloo world: ITS plan from the C++ runtime (tpl_plan_create — the
+    code an RCCL rank runs before capturing its graphs), exchanged with the other ranks'."""
+    import torch.distributed as tdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import tpl_amd
+        a = load_kkt(arcs, tmp).a
+        p = tpl_amd.HostPlan(a, mode=mode, nranks=world, rank=rank)
+        s = p.schedule()
+        mine = {"rows": p.local_rows.copy(), "s_short": s["short_rows"], "s_long": s["long_rows"],
+                "s_G2": s["G2"], "s_E": s["E"], "s_slices": s["slices"], "perm": s["perm"]}
+        p.close()
+        recs = [None] * world
+        tdist.all_gather_object(recs, mine)
+        if rank == 0:
+            import pickle
+            with open(os.path.join(tmp, f"plans_{mode}_{world}.pkl"), "wb") as f:
+                pickle.dump(recs, f)
+    finally:
+        tdist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["replicated", "rows"])
+def test_rank_plans_over_gloo(kkt_tmp, mode):
+    """World 2 over gloo, each rank its own process: the runtime's per-rank plans cover
+    every row exactly once (replicated mode: the long rows on every rank), hold no device
+    permutation, and drive the partition oracle (tests/partition_oracle.py — the order the
+    GPU ranks reduce in) to the same bits as plans made in one process."""
+    import pickle
+
+    import torch.multiprocessing as mp
+    from partition_oracle import PartitionOracle
+    sys.path.insert(0, os.path.join(HERE, "golden"))
+    from make_parity import digest, plan_records
+    world, arcs = 2, 50000
+    mp.spawn(_plan_worker, args=(world, _free_port(), kkt_tmp, arcs, mode), nprocs=world, join=True)
+    with open(os.path.join(kkt_tmp, f"plans_{mode}_{world}.pkl"), "rb") as f:
+        recs = pickle.load(f)  # written by this test's own rank 0 above
+    a = load_kkt(arcs, kkt_tmp).a
+    n = a.shape[0]
+    assert all(r["perm"] is None for r in recs)
+    rows = np.concatenate([r["rows"] for r in recs])
+    if mode == "rows":
+        assert np.array_equal(np.sort(rows), np.arange(n))
+    else:
+        assert np.array_equal(np.unique(rows), np.arange(n))
+    local = plan_records(a, mode, world)
+    for r, l in zip(recs, local):
+        for key in ("rows", "s_short", "s_long"):
+            assert np.array_equal(r[key], l[key]), key
+        assert (r["s_G2"], r["s_E"], r["s_slices"]) == (l["s_G2"], l["s_E"], l["s_slices"])
+    b = harness_b(a)
+    po = PartitionOracle(a, [{k: v for k, v in r.items() if k != "perm"} for r in recs], mode)
+    al, be, s, bn = po.pass_one(b, 20)
+    po1 = PartitionOracle(a, local, mode)
+    al1, be1, s1, bn1 = po1.pass_one(b, 20)
+    assert s == s1 and digest(al, be) == digest(al1, be1)
