@@ -238,20 +238,205 @@ def test_operator_input_is_copied_and_canonicalised():
     assert list(ci) == [0, 2, 1, 0] and list(v) == [5.0, 3.0, 0.0, 3.0]
 
 
-def test_rust_shim_binds_the_header():
-    """integration/rust/hip.rs (the reference crate's src/hip.rs; no Rust toolchain here)
-    declares only symbols include/tpl.h exports, each with the header's parameter count."""
-    src = open(os.path.join(ROOT, "integration", "rust", "hip.rs")).read()
-    block = src[src.index('extern "C" {\n    fn tpl_last_error_detail'):]
-    block = block[:block.index("\n}\n")]
-    rust = {m.group(1): m.group(2) for m in
-            re.finditer(r"fn (tpl_[a-z0-9_]+)\((.*?)\)\s*->", block, flags=re.S)}
-    hdr = open(os.path.join(ROOT, "include", "tpl.h")).read()
-    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    assert len(rust) >= 10
-    for name, params in rust.items():
-        m = re.search(rf"\b{name}\s*\((.*?)\);", hdr, flags=re.S)
-        assert m, name
-        n_h = 0 if m.group(1).strip() in ("", "void") else m.group(1).count(",") + 1
-        n_r = 0 if not params.strip() else params.count(",") + 1
-        assert n_h == n_r, (name, n_h, n_r)
+# ---- the Rust shim (integration/rust/hip.rs; no Rust toolchain in this image) ----------
+HIP_RS = os.path.join(ROOT, "integration", "rust", "hip.rs")
+REF_SRC = "/root/reference/src"
+
+# C type (base name) -> the Rust type an `extern "C"` binding must use for it
+_C_TO_RUST = {"double": "f64", "int": "c_int", "int32_t": "i32", "int64_t": "i64",
+              "uint64_t": "u64", "uint8_t": "u8", "size_t": "usize", "char": "c_char",
+              "void": "c_void", "tpl_status": "c_int", "tpl_ctx_t": "*mut TplCtx",
+              "tpl_op_t": "*mut TplOp", "tpl_ftk_fn": "FtkFn",
+              # the step callback is optional (NULL = none): a nullable fn pointer
+              "tpl_step_cb": "Option<StepCb>", "tpl_error_detail": "TplErrorDetail"}
+
+
+def _c_header():
+    return re.sub(r"/\*.*?\*/", "", open(os.path.join(ROOT, "include", "tpl.h")).read(),
+                  flags=re.S)
+
+
+def _split_top(s, sep=","):
+    """Split at `sep` outside (), <>, [] (Rust generics and C parameter lists)."""
+    out, depth, cur = [], 0, ""
+    for i, ch in enumerate(s):
+        if ch in "(<[":
+            depth += 1
+        elif ch in ")]" or (ch == ">" and not (i > 0 and s[i - 1] == "-")):
+            depth -= 1
+        if ch == sep and depth == 0:
+            out.append(cur)
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur)
+    return [p.strip() for p in out]
+
+
+def _c_type_to_rust(ctype):
+    """'const double*' -> '*const f64', 'tpl_ctx_t*' -> '*mut *mut TplCtx', ..."""
+    t = ctype.replace("*", " * ").split()
+    stars = t.count("*")
+    const = "const" in t
+    base = [w for w in t if w not in ("*", "const")]
+    assert len(base) == 1, ctype
+    rust = _C_TO_RUST[base[0]]
+    for lvl in range(stars):
+        rust = ("*const " if const and lvl == 0 else "*mut ") + rust
+    return rust
+
+
+def _c_params(plist, named=True):
+    if plist.strip() in ("", "void"):
+        return []
+    out = []
+    for p in _split_top(plist):
+        p = p.replace("*", "* ")
+        if named:
+            p = re.sub(r"\b[A-Za-z_][A-Za-z0-9_]*\s*$", "", p)  # drop the parameter name
+        out.append(_c_type_to_rust(p))
+    return out
+
+
+def _rust_norm(t):
+    return re.sub(r"\s+", "", t).replace("*const", "*const ").replace("*mut", "*mut ")
+
+
+def _extern_block():
+    src = open(HIP_RS).read()
+    block = src[src.index('extern "C" {'):]
+    return src, block[:block.index("\n}\n")]
+
+
+def test_rust_shim_extern_types_match_header():
+    """Every `extern "C"` item of hip.rs is a symbol of include/tpl.h whose parameter and
+    return TYPES are the header's, parameter by parameter (C -> Rust: const T* ->
+    *const T, T* -> *mut T, handles -> *mut opaque, size_t -> usize, tpl_status -> c_int,
+    the nullable step callback -> Option<fn>)."""
+    _, block = _extern_block()
+    hdr = _c_header()
+    items = list(re.finditer(r"fn (tpl_[a-z0-9_]+)\((.*?)\)\s*->\s*([^;]+);", block, flags=re.S))
+    assert len(items) >= 12
+    for m in items:
+        name, params, ret = m.group(1), m.group(2), m.group(3)
+        h = re.search(rf"\n\s*([A-Za-z_][A-Za-z0-9_ ]*?\**)\s*\b{name}\s*\((.*?)\);", hdr, flags=re.S)
+        assert h, name
+        want = _c_params(h.group(2))
+        got = [_rust_norm(p.split(":", 1)[1]) for p in _split_top(params)]
+        assert got == [_rust_norm(w) for w in want], (name, got, want)
+        assert _rust_norm(ret) == _rust_norm(_c_type_to_rust(h.group(1).strip())), name
+    # the ones VERDICT r04 found missing
+    names = {m.group(1) for m in items}
+    assert {"tpl_lanczos_standard", "tpl_copy_to_host", "tpl_lanczos_pass_two"} <= names
+
+
+def test_rust_shim_callback_and_struct_types_match_header():
+    """FtkFn / StepCb carry tpl_ftk_fn / tpl_step_cb's parameter types in order, and the
+    #[repr(C)] TplErrorDetail has tpl_error_detail's fields, names and types in order."""
+    src, _ = _extern_block()
+    hdr = _c_header()
+    for rust_name, c_name in (("FtkFn", "tpl_ftk_fn"), ("StepCb", "tpl_step_cb")):
+        r = re.search(rf'type {rust_name} = unsafe extern "C" fn\((.*?)\)\s*->\s*([^;]+);',
+                      src, flags=re.S)
+        c = re.search(rf"typedef\s+(\w+)\s*\(\*{c_name}\)\((.*?)\);", hdr, flags=re.S)
+        assert r and c, rust_name
+        assert [_rust_norm(p) for p in _split_top(r.group(1))] == \
+            [_rust_norm(p) for p in _c_params(c.group(2))], rust_name
+        assert _rust_norm(r.group(2)) == _c_type_to_rust(c.group(1))
+    r = re.search(r"#\[repr\(C\)\]\s*struct TplErrorDetail \{(.*?)\}", src, flags=re.S)
+    c = re.search(r"typedef struct tpl_error_detail \{(.*?)\}", hdr, flags=re.S)
+    rust_fields = [tuple(_rust_norm(x) for x in f.split(":")) for f in _split_top(r.group(1))]
+    c_fields = []
+    for decl in c.group(1).split(";"):
+        decl = decl.strip()
+        if not decl:
+            continue
+        first, *rest = [d.strip() for d in decl.split(",")]
+        m = re.match(r"(.*?)\b([A-Za-z_]\w*)$", first.replace("*", "* "))
+        ctype = m.group(1).strip()
+        for nm in [m.group(2)] + rest:
+            c_fields.append((nm, _rust_norm(_c_type_to_rust(ctype))))
+    assert rust_fields == c_fields
+
+
+def _rust_fns(src):
+    """name -> (generics, [(param, type)], return type, where clause) of every `pub fn`."""
+    src = re.sub(r"//[^\n]*", "", src)
+    out = {}
+    for m in re.finditer(r"\bpub fn (\w+)", src):
+        i = m.end()
+        gen = ""
+        if src[i] == "<":
+            d, j = 0, i
+            while True:
+                d += {"<": 1, ">": -1}.get(src[j], 0)
+                j += 1
+                if d == 0:
+                    break
+            gen, i = src[i + 1:j - 1], j
+        assert src[i] == "(", m.group(1)
+        d, j = 0, i
+        while True:
+            d += {"(": 1, ")": -1}.get(src[j], 0)
+            j += 1
+            if d == 0:
+                break
+        params = [(re.sub(r"^mut\s+", "", p.split(":", 1)[0].strip()), p.split(":", 1)[1])
+                  if ":" in p else (p, p)  # a `&self` receiver
+                  for p in _split_top(src[i + 1:j - 1])]
+        tail = src[j:src.index("{", j)]
+        ret = re.search(r"->\s*(.*?)\s*(?:\bwhere\b|$)", tail, flags=re.S).group(1)
+        where = tail.split("where", 1)[1] if "where" in tail else ""
+        out[m.group(1)] = (gen, params, ret, where)
+    return out
+
+
+def _sig_norm(t):
+    """The reference's generic scalar and operator read as the shim's concrete ones."""
+    t = re.sub(r"\s+", "", t)
+    t = re.sub(r"<TasComplexField>::Real|T::Real", "f64", t)
+    t = re.sub(r"\bT\b", "f64", t)
+    t = re.sub(r"^&(implLinOp<f64>|implHipOperand|O)$", "&OPERAND", t)
+    return t
+
+
+def _closure_bound(gen, where):
+    m = re.search(r"F:\s*(FnMut\(.*?\)\s*->\s*Result<[^{]*?anyhow::Error>)", gen + "," + where,
+                  flags=re.S)
+    return _sig_norm(m.group(1)) if m else None
+
+
+def test_rust_shim_signatures_match_reference():
+    """every public function of src/solvers.rs and
+    src/algorithms/{lanczos,lanczos_two_pass}.rs has a same-name counterpart in hip.rs with
+    the same parameter names in the same order (`stack: &mut MemStack` included), the same
+    parameter, closure-bound and return types once the reference's generic scalar T (and
+    T::Real) is read as f64 and its `LinOp<T>` operator as the shim's HipOperand; the
+    output structs and the callback type are the crate's own (imported, not redefined);
+    and HipCsrOp implements faer's LinOp<f64>."""
+    if not os.path.isdir(REF_SRC):
+        pytest.skip("reference checkout not present (GPU box)")
+    shim_src = open(HIP_RS).read()
+    shim = _rust_fns(shim_src)
+    ref = {}
+    for rel in ("solvers.rs", "algorithms/lanczos.rs", "algorithms/lanczos_two_pass.rs"):
+        ref.update(_rust_fns(open(os.path.join(REF_SRC, rel)).read()))
+    assert set(ref) == {"lanczos", "lanczos_two_pass", "lanczos_standard", "lanczos_pass_one",
+                        "lanczos_pass_two", "lanczos_pass_two_with_basis"}
+    for name, (gen, params, ret, where) in ref.items():
+        assert name in shim, name
+        sgen, sparams, sret, swhere = shim[name]
+        assert [p for p, _ in sparams] == [p for p, _ in params], name
+        assert [_sig_norm(t) for _, t in sparams] == [_sig_norm(t) for _, t in params], name
+        assert _sig_norm(sret) == _sig_norm(ret), name
+        assert _closure_bound(sgen, swhere) == _closure_bound(gen, where), name
+    for ty in ("LanczosCallback", "LanczosDecomposition", "LanczosOutput",
+               "LanczosPassTwoOutput", "TridiagonalSystemView"):
+        assert re.search(rf"use crate::algorithms::\{{[^}}]*\b{ty}\b", shim_src), ty
+        assert not re.search(rf"\b(struct|type) {ty}\b", shim_src), ty
+    assert re.search(r"impl LinOp<f64> for HipCsrOp", shim_src)
+    for m in ("apply_scratch", "nrows", "ncols", "apply", "conj_apply"):
+        assert re.search(rf"impl LinOp<f64> for HipCsrOp \{{.*?\bfn {m}\(", shim_src, flags=re.S), m
+    # the reference's own call sites pass `&a.as_ref()` (a SparseColMatRef)
+    assert re.search(r"impl<'a> HipOperand for SparseColMatRef<'a, usize, f64>", shim_src)
