@@ -104,6 +104,9 @@ def parse(argv=None):
     p.add_argument("--pcie", type=int, default=1, help="N=1: also time host b / x (PCIe)")
     p.add_argument("--parity", type=int, default=1,
                    help="0 to skip the parity block (digests vs tests/golden/parity.json)")
+    p.add_argument("--dist-mode", choices=("auto", "replicated", "rows"), default="auto",
+                   help="partition of the N > 1 solve: replicated long rows (auto: when the "
+                        "matrix allows it) or row blocks with the whole vector all-gathered")
     p.add_argument("--child-timeout", type=float, default=CHILD_TIMEOUT_S,
                    help="N>1: seconds the parent waits for the torchrun child")
     return p.parse_args(argv)
@@ -199,11 +202,26 @@ def parity_entry(expected: dict, name: str, **got) -> dict:
     return ent
 
 
+KERNEL_SOURCES = ("tpl_kernels.hip", "tpl_kcommon.h", "tpl_device.h", "tpl_lab.h")
+
+
+def kernel_src_digest() -> str:
+    """sha256 (16 hex digits) of the device-code sources in this tree: ties a committed
+    profile to the kernels it measured (scripts/update_profiles.py stores the same)."""
+    import hashlib
+    h = hashlib.sha256()
+    for name in KERNEL_SOURCES:
+        with open(os.path.join(ROOT, "two-pass-lanczos_amd", "csrc", name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def rocprof_spmv(steps: int, b_spmv: float):
-    """In-graph average duration of both SpMV kernels from the committed rocprofv3 summary
-    of the headline (profiles/rocprof_headline.json, scripts/update_profiles.py): their
-    fractions of the HBM roofline by B_spmv, and the time-weighted one over all 2k - 1
-    SpMV launches of a solve (k of k_p1_spmv, k - 1 of k_p2_spmv)."""
+    """COMMITTED profile, not this run: in-graph durations of both SpMV kernels from the
+    rocprofv3 summary of the headline (profiles/rocprof_headline.json, written by
+    scripts/update_profiles.py): their fractions of the HBM roofline by B_spmv, and the
+    time-weighted one over all 2k - 1 SpMV launches of a solve (k of k_p1_spmv, k - 1 of
+    k_p2_spmv). `matches_build` says whether that profile measured this tree's kernels."""
     path = os.path.join(ROOT, "profiles", "rocprof_headline.json")
     try:
         with open(path) as f:
@@ -211,7 +229,8 @@ def rocprof_spmv(steps: int, b_spmv: float):
     except (OSError, ValueError):
         return None
     frac = lambda ns: round(b_spmv / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4)
-    out = {"source": rj.get("source")}
+    out = {"source": rj.get("source"), "kernel_src_sha16": rj.get("kernel_src_sha16"),
+           "matches_build": rj.get("kernel_src_sha16") == kernel_src_digest()}
     # mean (rocprofv3 --stats) and median ("median per-kernel time")
     for stat, key in (("mean", "avg_ns"), ("median", "median_ns")):
         try:
@@ -222,7 +241,93 @@ def rocprof_spmv(steps: int, b_spmv: float):
         out[stat] = {"k_p1_spmv_us": round(t1 / 1000, 3), "k_p1_spmv_frac": frac(t1),
                      "k_p2_spmv_us": round(t2 / 1000, 3), "k_p2_spmv_frac": frac(t2),
                      "all_spmv_time_weighted_frac": round(tw / HBM_PEAK_GBS, 4)}
-    return out if len(out) > 1 else None
+    return out if len(out) > 3 else None
+
+
+def roofline_block(b_spmv, b_fused, p2_us, p1s_us, p1a_us, n_samp, steps, p1_step_us,
+                   solve_s, p2_traffic, p2_traffic_src, p1_traffic, p1_traffic_src, iso,
+                   partitioned):
+    """The line's `roofline`: the DOMINANT kernel by live time share (k_p1_spmv: k launches
+    per solve; k_p2_spmv: k - 1; both measured live with HIP events in the timed solves —
+    k_p2_spmv over the whole pass-two graph, k_p1_spmv over 8 sampled steps of pass one),
+    SURVEY.md §8(d)'s B_spmv over its average launch time vs 8 TB/s (`frac`), its PMC
+    counter bytes (`traffic`) and the fraction those bytes make of peak in the same time
+    (`frac_counter_bytes`); the other SpMV and the time-weighted figure over all 2k - 1
+    SpMV launches beside it."""
+    gbs = lambda byts, t_us: byts / (t_us * 1e-6) / 1e9
+    frac = lambda byts, t_us: round(gbs(byts, t_us) / HBM_PEAK_GBS, 4)
+    kern = {"k_p2_spmv": {"avg_launch_us_events": round(p2_us, 3), "launches_per_solve": steps - 1,
+                          "events": "one pair around the graph of the pass-two step launches",
+                          "achieved": round(gbs(b_spmv, p2_us), 1), "frac": frac(b_spmv, p2_us),
+                          "traffic": p2_traffic, "traffic_source": p2_traffic_src,
+                          "fused_bytes_per_launch": b_fused,
+                          "frac_fused_bytes": frac(b_fused, p2_us)}}
+    if p1s_us:
+        t1 = (p1_traffic or {}).get("k_p1_spmv")
+        kern["k_p1_spmv"] = {"avg_launch_us_events": round(p1s_us, 3), "launches_per_solve": steps,
+                             "events": f"around {n_samp} sampled steps' launches in the pass-one graph",
+                             "achieved": round(gbs(b_spmv, p1s_us), 1), "frac": frac(b_spmv, p1s_us),
+                             "traffic": t1, "traffic_source": p1_traffic_src}
+        kern["k_p1_axpy"] = {"avg_launch_us_events": round(p1a_us, 3), "launches_per_solve": steps,
+                             "traffic": (p1_traffic or {}).get("k_p1_axpy")}
+    for name, kd in kern.items():
+        if kd.get("traffic"):
+            kd["frac_counter_bytes"] = frac(kd["traffic"], kd["avg_launch_us_events"])
+    spmv = [n for n in ("k_p1_spmv", "k_p2_spmv") if n in kern]
+    dom = max(spmv, key=lambda n: kern[n]["avg_launch_us_events"] * kern[n]["launches_per_solve"])
+    d = kern[dom]
+    out = {"bound": "hbm", "kernel": dom + ("" if not partitioned else " (+ exchange, rank 0)"),
+           "achieved": d["achieved"], "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": d["frac"],
+           "traffic": d.get("traffic"), "traffic_source": d.get("traffic_source"),
+           "frac_counter_bytes": d.get("frac_counter_bytes"),
+           "bytes_per_launch": b_spmv,
+           "bytes_rule": "SURVEY.md §8(d) B_spmv = 12 nnz + 4 (n+1) + 16 n",
+           "avg_launch_us_events": d["avg_launch_us_events"],
+           "dominant_by": "live time share: avg launch (events) x launches per solve",
+           "kernels": kern,
+           "pass1_us_per_step": round(p1_step_us, 3),
+           "frac_pass1_step": frac(b_spmv, p1_step_us),
+           "frac_whole_solve": round((2 * steps - 1) * b_spmv / solve_s / 1e9 / HBM_PEAK_GBS, 4),
+           "kernels_us_isolated": iso}
+    if p1s_us:
+        out["all_spmv_time_weighted_frac"] = round(
+            (2 * steps - 1) * b_spmv / ((steps * p1s_us + (steps - 1) * p2_us) * 1e-6) / 1e9
+            / HBM_PEAK_GBS, 4)
+    return out
+
+
+RANK_SHARE_FILE = os.path.join(ROOT, "profiles", "rank_share.json")
+
+
+def predicted_block(world: int, k: int, steps: int, solve_s: float):
+    """The prediction an N-rank line is held against (scripts/rank_share.py, committed as
+    profiles/rank_share.json): rank 0's share of the replicated partition at this N, solved
+    on one GPU through one RCCL rank — every kernel one rank runs per step, with
+    collectives that move nothing — plus (2 k + k - 1) all-gathers per solve at an unknown
+    latency L each. Beside the measured time: the L it implies."""
+    try:
+        with open(RANK_SHARE_FILE) as f:
+            rs = json.load(f)
+        sh = rs["shares"][str(world)]
+    except (OSError, ValueError, KeyError):
+        return None
+    one = sh["one_rank_replicated"]
+    if rs.get("k") != k or one.get("steps") != steps:
+        return {"error": f"profile is for k={rs.get('k')}, steps={one.get('steps')}"}
+    c = 2 * steps + (steps - 1)
+    t0 = one["ms_per_solve"]
+    return {"source": f"profiles/rank_share.json ({rs.get('source', 'scripts/rank_share.py')})",
+            "rank0_rows": sh["rank0_rows"], "rank0_nnz": sh["rank0_nnz"],
+            "per_step_us_1rank": {"pass1": one["pass1_us_per_step"],
+                                  "pass2": one["pass2_us_per_step"]},
+            "exchange_1rank_us": one.get("exchange_1rank_us"),
+            "single_gpu_same_share_ms": sh.get("single_gpu", {}).get("ms_per_solve"),
+            "collectives_per_step": sh["collectives_per_step"], "collectives_per_solve": c,
+            "model": "ms = ms_1rank + collectives_per_solve * L / 1000",
+            "ms_1rank": t0,
+            "ms_at_L_us": {str(L): round(t0 + c * L / 1000.0, 3) for L in (5, 10, 20, 40)},
+            "measured_ms": round(1000.0 * solve_s, 3),
+            "implied_L_us": round((1000.0 * solve_s - t0) * 1000.0 / c, 2)}
 
 
 # ---- N > 1: the parent process (never touches the GPU) ------------------------------
@@ -371,7 +476,7 @@ def main():
         dctx = DistContext(rank, world, device=device,
                            transport=os.environ.get("TPL_DIST_TRANSPORT", "rccl"))
         stage_marker("comm_init")
-        op = DistHipCsrOp(a, dctx)
+        op = DistHipCsrOp(a, dctx, mode=args.dist_mode)
         b_loc = op.local(b)
     stage_marker("operator")
     b_dev = torch.from_numpy(np.ascontiguousarray(b_loc)).cuda(device)
@@ -426,6 +531,13 @@ def main():
     b_fused = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
     achieved = b_spmv / (us * 1e-6) / 1e9
     p1_step_us = p1_us / steps_taken
+    # pass one's kernels, live in the graph: events around k_p1_spmv and k_p1_axpy of 8
+    # sampled steps of the last timed solve (single GPU, one-graph solve)
+    try:
+        s1_us, a1_us, n_samp = op.step_samples()
+    except Exception:  # noqa: BLE001 - partitioned / host f: no sampled pass one
+        s1_us = a1_us = None
+        n_samp = 0
     solve_s = dt / args.steps
     # isolated per-kernel event timings (graph of back-to-back launches), diagnostics only
     names = {_lib.TPL_KERNEL_PASS1_SPMV: "k_p1_spmv", _lib.TPL_KERNEL_PASS1_AXPY: "k_p1_axpy",
@@ -442,12 +554,14 @@ def main():
             pj = json.load(f)
         traffic, traffic_src = pj["traffic_bytes_per_launch"], pj["source"]
 
-    p1_traffic = None
+    p1_traffic, p1_traffic_src = None, None
     pmc1 = os.path.join(ROOT, "profiles", "pmc_pass_one.json")
     if os.path.exists(pmc1) and arcs == 500000 and not partitioned and args.k == 500:
         with open(pmc1) as f:
-            p1_traffic = {k.split("::")[-1]: v["traffic_bytes_per_launch"]
-                          for k, v in json.load(f)["kernels"].items()}
+            pj1 = json.load(f)
+        p1_traffic = {k.split("::")[-1].split("<")[0]: v["traffic_bytes_per_launch"]
+                      for k, v in pj1["kernels"].items()}
+        p1_traffic_src = pj1.get("source")
     iters = args.steps * steps_taken
     value = iters / dt
     x_host = x_dev.cpu().numpy()
@@ -541,27 +655,14 @@ def main():
                    else (f"{op.mode}{world} (" + ("long-row partials all-gathered per SpMV"
                          if op.mode == "replicated" else "vector all-gathered per SpMV")
                          + f", {dctx.transport})")},
-        "roofline": {"bound": "hbm", "kernel": "k_p2_spmv" + ("" if not partitioned else
-                                                             " (+ exchange, rank 0)"),
-                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": traffic, "traffic_source": traffic_src,
-                     "bytes_per_launch": b_spmv,
-                     "bytes_rule": "SURVEY.md §8(d) B_spmv = 12 nnz + 4 (n+1) + 16 n",
-                     "avg_launch_us_events": round(us, 3),
-                     "fused_bytes_per_launch": b_fused,
-                     "frac_fused_bytes": round(b_fused / (us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                     "pass1_us_per_step": round(p1_step_us, 3),
-                     "frac_pass1_step": round(b_spmv / (p1_step_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
-                     "pass1_traffic_per_launch": p1_traffic,
-                     "frac_whole_solve": round((2 * steps_taken - 1) * b_spmv / solve_s / 1e9
-                                               / HBM_PEAK_GBS, 4),
-                     "kernels_us_isolated": iso},
+        "roofline": roofline_block(b_spmv, b_fused, us, s1_us, a1_us, n_samp, steps_taken,
+                                   p1_step_us, solve_s, traffic, traffic_src, p1_traffic,
+                                   p1_traffic_src, iso, partitioned),
     }
 
     rp = rocprof_spmv(steps_taken, b_spmv) if (arcs == 500000 and not partitioned) else None
     if rp is not None:
-        out["roofline"]["spmv_kernels_rocprof"] = rp
+        out["roofline"]["committed_profile"] = rp
     if single is not None:
         out["single_gpu_same_workload"] = single
     if partitioned:
@@ -579,6 +680,10 @@ def main():
                                "comm_frac": round(comm_ms / (1000.0 * solve_s), 4)}
         except Exception as e:  # noqa: BLE001
             out["exchange"] = {"error": str(e)}
+    if partitioned and world > 1 and op.mode == "replicated" and rank == 0:
+        pred = predicted_block(world, args.k, steps_taken, solve_s)
+        if pred is not None:
+            out["predicted"] = pred
     if args.pcie and not partitioned and world == 1:
         # PCIe-inclusive rate (never `value`): host b in, host x out, one H2D + one D2H
         xh = np.empty(n)

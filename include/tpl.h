@@ -335,6 +335,13 @@ tpl_status tpl_op_device_bytes(tpl_op_t op, uint64_t* bytes);
 tpl_status tpl_op_enable_timing(tpl_op_t op, int on);
 tpl_status tpl_op_pass_timing(tpl_op_t op, double* pass1_us, double* pass2_spmv_us,
                               int64_t* pass2_launches);
+/* Live in-graph durations of pass one's two kernels: with timing on, the pass one of a
+ * single-GPU one-graph solve (tpl_lanczos_two_pass with a device f, k >= 16) records HIP
+ * events around k_p1_spmv and k_p1_axpy of 8 steps spread over the pass; this returns
+ * their averages over the samples of the last timed solve (event to event: each includes
+ * its launch's boundary, like pass2_spmv_us).                                     */
+tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_us,
+                               int32_t* samples);
 
 /* ---- row-partitioned operator over several GPUs ----------
  * One process per GPU. Rank r holds the rows [starts[r], starts[r+1]) of A; every

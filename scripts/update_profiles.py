@@ -66,7 +66,7 @@ with open(os.path.join(prof, "pmc_pass_one.json"), "w") as f:
     json.dump(p1, f, indent=1)
 print(p1)
 # in-graph average duration of both SpMV kernels of the headline (rocprofv3 --stats of
-# the --headline-only run): bench.py reads it for roofline.spmv_kernels_rocprof
+# the --headline-only run): bench.py reads it for roofline.committed_profile
 stats = {}
 import csv
 with open(os.path.join(out, "prof", "run_kernel_stats.csv")) as f:
@@ -82,7 +82,9 @@ if os.path.exists(mpath):
         for k in ("k_p1_spmv<58>", "k_p2_spmv<58>", "k_p1_axpy<12>"):
             if name == k:
                 med[k.split("<")[0]] = round(1000.0 * v["median_us"], 1)
-rj = {"config": CFG, "avg_ns": {k: v["avg_ns"] for k, v in stats.items()}, "median_ns": med,
+sys.path.insert(0, ROOT)
+from bench import kernel_src_digest  # noqa: E402  (the profile's kernels: this tree's)
+rj = {"config": CFG, "kernel_src_sha16": kernel_src_digest(), "avg_ns": {k: v["avg_ns"] for k, v in stats.items()}, "median_ns": med,
       "calls": {k: v["calls"] for k, v in stats.items()},
       "percentage_of_gpu_time": {k: v["percentage"] for k, v in stats.items()},
       "source": f"profiles/{tag}_kernel_stats.csv (rocprofv3 --kernel-trace --stats, bench.py "

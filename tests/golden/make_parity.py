@@ -62,6 +62,14 @@ WORKLOADS = {
                                    mode="replicated", nranks=4),
     "configs4_replicated_N8": dict(arcs=5000000, k=500, f="inv", solver="partition",
                                    mode="replicated", nranks=8),
+    # the row-block partition (bench.py --gpus N with TPL_DIST_MODE=rows): every SpMV
+    # all-gathers the whole vector
+    "configs4_rows_N2": dict(arcs=5000000, k=500, f="inv", solver="partition", mode="rows",
+                             nranks=2),
+    "configs4_rows_N4": dict(arcs=5000000, k=500, f="inv", solver="partition", mode="rows",
+                             nranks=4),
+    "configs4_rows_N8": dict(arcs=5000000, k=500, f="inv", solver="partition", mode="rows",
+                             nranks=8),
 }
 # quick cases the CPU suite recomputes every run (the same code paths at a small k)
 QUICK = {
@@ -71,6 +79,10 @@ QUICK = {
                                        mode="replicated", nranks=8),
     "configs4_rows_N2_k20": dict(arcs=5000000, k=20, f="inv", solver="partition",
                                  mode="rows", nranks=2),
+    "configs4_rows_N4_k20": dict(arcs=5000000, k=20, f="inv", solver="partition",
+                                 mode="rows", nranks=4),
+    "configs4_rows_N8_k20": dict(arcs=5000000, k=20, f="inv", solver="partition",
+                                 mode="rows", nranks=8),
 }
 
 

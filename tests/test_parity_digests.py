@@ -108,6 +108,6 @@ def test_partition_digests_recompute_k20(fixture, kkt_tmp, name):
 @pytest.mark.skipif(not FULL, reason="minutes per case: TPL_PARITY_FULL=1")
 @pytest.mark.parametrize("name", [n for n in make_parity.WORKLOADS
                                   if n.startswith(("configs3_cgs2", "configs3_selective",
-                                                   "configs4_replicated"))])
+                                                   "configs4_replicated", "configs4_rows"))])
 def test_full_digests_recompute(fixture, kkt_tmp, name):
     _check(name, make_parity.WORKLOADS[name], fixture["workloads"][name], kkt_tmp)

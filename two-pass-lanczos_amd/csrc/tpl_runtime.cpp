@@ -37,8 +37,11 @@ hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStrea
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
 // elim: one more workgroup eliminates row j - 3 of T_k's LU (one-graph inv)
+// tot != nullptr (replicated partition): the last workgroup also reduces the G2 norm
+// partials into *tot, this rank's beta total (cnt: its arrival counter, zero between launches)
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
-                   double* r_next, int j, int k, int elim, hipStream_t s);
+                   double* r_next, int j, int k, int elim, hipStream_t s, double* tot = nullptr,
+                   unsigned int* cnt = nullptr);
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
 hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
                    const int32_t* idx, hipStream_t s);
@@ -124,7 +127,13 @@ enum GraphKind {
   kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
   kGPass1Elim = 7,    // (timed variant) pass one eliminating T_k's LU as it goes
   kGStandardElim = 8, // the standard pass eliminating T_k's LU as it goes (one-pass inv)
+  kGPass1Sampled = 9, // (timed variant) pass one with events around sampled steps' kernels
+  kGPass1ElimSampled = 10,
 };
+// Live in-graph timing of pass one's two kernels (tpl_op_step_samples): with timing on, a
+// single-GPU one-graph solve's pass one records events around k_p1_spmv and k_p1_axpy of
+// kStepSamples steps spread over the pass (step 1 + (2i + 1) k / (2 kStepSamples)).
+constexpr int kStepSamples = 8;
 // Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
 // run ahead of the host callback.
 constexpr int kCbBatchMax = 32;
@@ -202,6 +211,8 @@ struct tpl_op_s {
   double *bG = nullptr, *RG[3] = {nullptr, nullptr, nullptr}, *V2G[3] = {nullptr, nullptr, nullptr},
          *tmpG = nullptr;
   double* d_rsum = nullptr;         // [nranks alpha totals][nranks norm totals] (partition)
+  unsigned int* d_bcnt = nullptr;   // k_p1_axpy's arrival counter (replicated partition: the
+                                    // beta rank total folded into it), its own 128-B line
   // solver state
   size_t kcap = 0;
   void* d_state = nullptr;  // flags | norms | alphas | betas | y | Pa | Pb | Pr
@@ -232,6 +243,9 @@ struct tpl_op_s {
   size_t vext_cols = 0;
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
+  // sampled pass-one steps: [i][0] before k_p1_spmv, [1] between, [2] after k_p1_axpy
+  hipEvent_t sev[kStepSamples][3] = {};
+  int p1_samples = 0;               // samples recorded by the last timed solve
   // tpl_plan_create: the host half of an operator only (rows, order, layout), for the
   // oracle's reduction order without a GPU; every device entry point refuses it
   bool plan_only = false;
@@ -630,9 +644,14 @@ void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
     dist_allgather(op, op->d_rsum, 1);
   }
 }
+// Replicated partition: k_p1_axpy's last workgroup reduces the rank's beta total (its
+// register tree holds up to 1024 partials, the default max_g2); else a separate launch.
+bool beta_folded(const tpl_op_s* op, const CsrDev& A) { return op->hybrid && A.G2 <= 1024; }
+
 void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
   if (op->hybrid) {
-    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+    if (!beta_folded(op, A))
+      dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
     dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
   } else {
     const int R = op->dist->nranks;
@@ -655,25 +674,42 @@ void enqueue_p2_exchange(tpl_op_s* op, int j) {
 
 // Pass one, step j (k = requested steps). elim: also eliminate row j - 3 of T_k's LU
 // (the one-graph inv, k_p1_axpy).
-void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false) {
+// sample >= 0: record the sample's events around the step's two kernels (single GPU).
+void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false,
+                     int sample = -1) {
   const CsrDev A = csr_dev(op, true);
+  if (sample >= 0) HIPCHK(hipEventRecord(op->sev[sample][0], op->stream));
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
                          op->W, Vcol, j, op->stream));
+  if (sample >= 0) HIPCHK(hipEventRecord(op->sev[sample][1], op->stream));
   if (op->dist) enqueue_p1_exchange_a(op, A);
   if (op->hybrid)
     HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, op->dist->nranks, r_of(op, j),
                                j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol,
                                op->d_rsum + op->dist->nranks, j, op->stream));
+  // replicated partition: the beta rank total is reduced by k_p1_axpy's last workgroup
+  double* btot = (beta_folded(op, A) && j < k)
+                     ? const_cast<double*>(op->S.Pb_r) + op->dist->rank : nullptr;
   HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k,
-                         elim ? 1 : 0, op->stream));
+                         elim ? 1 : 0, op->stream, btot, btot ? op->d_bcnt : nullptr));
+  if (sample >= 0) HIPCHK(hipEventRecord(op->sev[sample][2], op->stream));
   if (op->dist && j < k) enqueue_p1_exchange_b(op, A, j);
 }
 
-void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false) {
+// The sample index of step j of a k-step sampled pass one, or -1.
+int step_sample(int j, int k) {
+  if (k < 2 * kStepSamples) return -1;
+  for (int i = 0; i < kStepSamples; ++i)
+    if (j == 1 + (2 * i + 1) * k / (2 * kStepSamples)) return i;
+  return -1;
+}
+
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false,
+                   bool sampled = false) {
   enqueue_p1_prologue(op);
   for (int j = 1; j <= (int)k; ++j) {
     double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
-    enqueue_p1_step(op, j, (int)k, Vcol, elim);
+    enqueue_p1_step(op, j, (int)k, Vcol, elim, sampled ? step_sample(j, (int)k) : -1);
     if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
   }
 }
@@ -830,7 +866,10 @@ void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
     return;
   }
   HIPCHK(hipEventRecord(op->tev[0], op->stream));
-  run_graph(op, elim ? kGPass1Elim : kGPass1, k, [&] { enqueue_pass1(op, k, false, false, elim); });
+  const bool sampled = !op->dist && k >= 2 * kStepSamples;
+  run_graph(op, sampled ? (elim ? kGPass1ElimSampled : kGPass1Sampled) : (elim ? kGPass1Elim : kGPass1),
+            k, [&] { enqueue_pass1(op, k, false, false, elim, sampled); });
+  op->p1_samples = sampled ? kStepSamples : 0;
   HIPCHK(hipEventRecord(op->tev[1], op->stream));
   run_graph(op, kGDevFtk, key, [&] { enqueue_ftk_dev(op, k, f); });
   HIPCHK(hipEventRecord(op->tev[2], op->stream));
@@ -929,8 +968,10 @@ void init_op(tpl_op_s* op) {
     // [nranks alpha totals | long-row alpha partials (hybrid) | nranks norm totals]
     const size_t nr = (size_t)op->dist->nranks;
     const size_t cnt = 2 * nr + (op->hybrid ? (size_t)long_epi_blocks(op) : 0);
-    dev_alloc(op, &op->d_rsum, cnt * sizeof(double));
-    HIPCHK(hipMemset(op->d_rsum, 0, cnt * sizeof(double)));
+    const size_t cnt_pad = (cnt + 15) / 16 * 16;  // the arrival counter on a 128-B line
+    dev_alloc(op, &op->d_rsum, (cnt_pad + 16) * sizeof(double));
+    HIPCHK(hipMemset(op->d_rsum, 0, (cnt_pad + 16) * sizeof(double)));
+    op->d_bcnt = reinterpret_cast<unsigned int*>(op->d_rsum + cnt_pad);
     if (op->hybrid) {
       // every rank's chunk count (each rank's short rows are a contiguous block of the
       // global split, chunked by kChunkRows: every rank computes all counts alike)
@@ -949,6 +990,8 @@ void init_op(tpl_op_s* op) {
   HIPCHK(hipEventCreate(&op->ev0));
   HIPCHK(hipEventCreate(&op->ev1));
   for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
+  for (auto& ev : op->sev)
+    for (hipEvent_t& e : ev) HIPCHK(hipEventCreate(&e));
 }
 
 // Contiguous blocks over items 0..m-1 with cost prefix[m+1]: cut where the prefix
@@ -1160,6 +1203,9 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     if (op->ev1) hipEventDestroy(op->ev1);
     for (hipEvent_t e : op->tev)
       if (e) hipEventDestroy(e);
+    for (auto& ev : op->sev)
+      for (hipEvent_t e : ev)
+        if (e) hipEventDestroy(e);
     delete op;
   });
 }
@@ -1638,6 +1684,30 @@ tpl_status tpl_op_enable_timing(tpl_op_t op, int on) {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     op->timing = on != 0;
     op->p2_launches = 0;
+    op->p1_samples = 0;
+  });
+}
+
+tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_us,
+                               int32_t* samples) {
+  return guarded([&] {
+    if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    if (!op->timing || op->p1_samples <= 0)
+      fail(TPL_ERR_INVALID_ARGUMENT,
+           "no sampled solve (enable timing, then run a one-graph two-pass solve with k >= 16)");
+    set_device(op);
+    HIPCHK(hipEventSynchronize(op->tev[1]));
+    double s = 0.0, a = 0.0;
+    for (int i = 0; i < op->p1_samples; ++i) {
+      float t0 = 0.f, t1 = 0.f;
+      HIPCHK(hipEventElapsedTime(&t0, op->sev[i][0], op->sev[i][1]));
+      HIPCHK(hipEventElapsedTime(&t1, op->sev[i][1], op->sev[i][2]));
+      s += t0;
+      a += t1;
+    }
+    if (p1_spmv_us) *p1_spmv_us = 1000.0 * s / op->p1_samples;
+    if (p1_axpy_us) *p1_axpy_us = 1000.0 * a / op->p1_samples;
+    if (samples) *samples = op->p1_samples;
   });
 }
 

@@ -117,6 +117,7 @@ tpl_kernel_algo_bytes = _sig("tpl_kernel_algo_bytes", c_double, c_void_p, c_int)
 tpl_copy_to_host = _sig("tpl_copy_to_host", c_int, c_void_p, c_void_p, c_size_t)
 tpl_op_enable_timing = _sig("tpl_op_enable_timing", c_int, c_void_p, c_int)
 tpl_op_pass_timing = _sig("tpl_op_pass_timing", c_int, c_void_p, PD, PD, POINTER(c_int64))
+tpl_op_step_samples = _sig("tpl_op_step_samples", c_int, c_void_p, PD, PD, POINTER(c_int32))
 tpl_op_set_device_ftk = _sig("tpl_op_set_device_ftk", c_int, c_void_p, c_int)
 tpl_op_device_bytes = _sig("tpl_op_device_bytes", c_int, c_void_p, POINTER(ctypes.c_uint64))
 tpl_op_set_reorder = _sig("tpl_op_set_reorder", c_int, c_void_p, c_int)
@@ -162,7 +163,7 @@ EXPORTED = [
     "tpl_lanczos_two_pass", "tpl_lanczos_standard", "tpl_lanczos_pass_one",
     "tpl_lanczos_pass_two", "tpl_load_kkt_system", "tpl_csr_host_free", "tpl_op_schedule",
     "tpl_op_set_schedule", "tpl_op_slices", "tpl_op_set_slices", "tpl_profile_kernel", "tpl_kernel_algo_bytes", "tpl_copy_to_host",
-    "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_generate_kkt", "tpl_op_flags",
+    "tpl_op_enable_timing", "tpl_op_pass_timing", "tpl_op_step_samples", "tpl_generate_kkt", "tpl_op_flags",
     "tpl_op_set_value_format", "tpl_op_set_device_ftk",
     "tpl_op_device_bytes", "tpl_op_reorth_second_passes", "tpl_op_set_reorder",
     "tpl_op_permutation", "tpl_locality_order", "tpl_op_tune_order",

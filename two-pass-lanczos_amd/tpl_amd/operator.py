@@ -288,6 +288,13 @@ class HipCsrOp:
         check(_lib.tpl_op_pass_timing(self._op, byref(p1), byref(p2), byref(n2)))
         return p1.value, p2.value, n2.value
 
+    def step_samples(self):
+        """-> (k_p1_spmv us, k_p1_axpy us, samples): live in-graph durations of pass one's
+        two kernels, averaged over the sampled steps of the last timed one-graph solve."""
+        s, a, n = c_double(), c_double(), c_int32()
+        check(_lib.tpl_op_step_samples(self._op, byref(s), byref(a), byref(n)))
+        return s.value, a.value, n.value
+
     def algo_bytes(self, kernel: int) -> float:
         return float(_lib.tpl_kernel_algo_bytes(self._op, kernel))
 
