@@ -339,9 +339,20 @@ def stage_marker(stage: str) -> None:
         return
     try:
         with open(os.path.join(d, f"rank{os.environ.get('RANK', '0')}.stage"), "a") as f:
-            f.write(f"{time.time():.3f} {os.getpid()} {stage}\n")
+            f.write(f"{time.time():.3f} {os.getpid()}:{proc_start(os.getpid())} {stage}\n")
     except OSError:
         pass
+
+
+def proc_start(pid: int) -> str:
+    """The process's start time in clock ticks since boot (/proc/PID/stat field 22): with
+    the pid it names one process, so a recorded rank is never confused with a later
+    process that reuses its pid. "" when unreadable."""
+    try:
+        with open(f"/proc/{pid}/stat") as f:
+            return f.read().rsplit(")", 1)[1].split()[19]
+    except (OSError, IndexError):
+        return ""
 
 
 def read_stages(d: str) -> dict:
@@ -360,16 +371,21 @@ def read_stages(d: str) -> dict:
         except OSError:
             continue
         if lines and all(len(ln) == 3 for ln in lines):
+            pid, _, start = lines[-1][1].partition(":")
             out[fn[len("rank"):-len(".stage")]] = {"stage": lines[-1][2], "stages": len(lines),
                                                    "t": float(lines[-1][0]),
-                                                   "pid": int(lines[-1][1])}
+                                                   "pid": int(pid), "start": start}
     return out
 
 
 def run_parent(argv, nproc: int, timeout: float, cmd=None) -> int:
     """Launch the N-rank child (torchrun; `cmd` overrides it for tests) in its own process
     group, wait at most `timeout` s; on a time-out or a failure kill the whole group and
-    print ONE JSON line naming the last stage each rank reached. Returns the exit status."""
+    print ONE JSON line naming the last stage each rank reached. Returns the exit status.
+    That line is the LAST line of the run and the authoritative one: a rank of a failing
+    child may have printed its own line before it (tests/test_bench_cli.py).
+    A rank recorded in the markers is killed only while its pid still names the same
+    process (its start time, /proc/PID/stat), never a later process reusing the pid."""
     import signal
     import tempfile
     d = tempfile.mkdtemp(prefix="tpl_bench_stages_")
@@ -399,12 +415,13 @@ def run_parent(argv, nproc: int, timeout: float, cmd=None) -> int:
                 continue
         stages = read_stages(d)
         for st in stages.values():
-            try:
-                os.kill(st["pid"], signal.SIGKILL)
-            except (ProcessLookupError, PermissionError):
-                pass
+            if st["start"] and proc_start(st["pid"]) == st["start"]:
+                try:
+                    os.kill(st["pid"], signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
             st["t"] = round(st["t"] - t0, 1)
-            del st["pid"]
+            del st["pid"], st["start"]
         print(json.dumps({"metric": METRIC, "value": None, "unit": "Lanczos iterations/s",
                           "n_gpus": nproc, "higher_is_better": True, "status": status,
                           "exit_code": rc, "child_timeout_s": timeout,

@@ -1,6 +1,7 @@
 """bench.py's driver contract on the CPU: argument plumbing and the N-GPU launcher
 (the parent starts torch.distributed.run as a child — never an exec, never a GPU call —
 and exits with its status)."""
+import json
 import os
 import sys
 
@@ -53,6 +54,9 @@ _STUB = r"""
 import os, subprocess, sys, time
 mode = sys.argv[1]
 if len(sys.argv) == 2:  # the launcher: start two ranks in sessions of their own (torchrun)
+    if os.environ.get("FAKE_PID"):  # a marker whose pid now names another process
+        with open(os.path.join(os.environ["TPL_BENCH_STAGE_DIR"], "rank9.stage"), "w") as f:
+            f.write(f"{time.time():.3f} {os.environ['FAKE_PID']}:1 start\n")
     ps = [subprocess.Popen([sys.executable, __file__, mode, str(r)], start_new_session=True,
                            env=dict(os.environ, RANK=str(r))) for r in range(2)]
     sys.exit(max(p.wait() for p in ps))
@@ -119,3 +123,23 @@ def test_rank_does_not_relaunch(monkeypatch):
 def test_host_info():
     h = bench.host_info()
     assert h["nproc"] >= 1 and h["allowed_cpus"] >= 1
+
+
+def test_parent_never_kills_a_reused_pid(tmp_path, capsys, monkeypatch):
+    """a rank pid in the markers is killed only while it still names the same
+    process (start time from /proc/PID/stat); a process that reuses the pid survives."""
+    import subprocess
+    assert bench.proc_start(os.getpid()) != ""
+    sleeper = subprocess.Popen(["sleep", "60"])
+    try:
+        stub = tmp_path / "stub.py"
+        stub.write_text(_STUB)
+        monkeypatch.setenv("BENCH_ROOT", ROOT)
+        monkeypatch.setenv("FAKE_PID", str(sleeper.pid))
+        assert bench.run_parent([], 2, 5.0, cmd=[sys.executable, str(stub), "fail"]) == 3
+        line = json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+        assert line["status"] == "failed" and "9" in line["last_stage"]
+        assert sleeper.poll() is None  # alive: its start time is not the recorded one
+    finally:
+        sleeper.kill()
+        sleeper.wait()

@@ -550,7 +550,9 @@ __global__ __launch_bounds__(kTPB) void k_ftk_inv(DevState S, int scale) {
   // Off the chain, on all lanes: the pivots' reciprocals, each row repacked as one
   // 32-B record {B, DU, DU2, D} (two 16-B LDS reads per row on the chain instead of four
   // 8-B ones), and div_rn's range test of every pivot and reciprocal.
-  double* P = sh + 7 * n;  // 4 (n - 1) doubles
+  // 4 (n - 1) doubles from an even offset: 16-B aligned records for the 16-B LDS accesses
+  // whatever the parity of n (at most 11 n - 3 <= 11 kcap doubles in all)
+  double* P = sh + ((7 * n + 1) & ~1);
   bool pbad = false;
   for (int i = threadIdx.x; i + 1 < n; i += kTPB) {
     const double d = D[i], r = 1.0 / d;
