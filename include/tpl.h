@@ -335,11 +335,11 @@ tpl_status tpl_op_device_bytes(tpl_op_t op, uint64_t* bytes);
 tpl_status tpl_op_enable_timing(tpl_op_t op, int on);
 tpl_status tpl_op_pass_timing(tpl_op_t op, double* pass1_us, double* pass2_spmv_us,
                               int64_t* pass2_launches);
-/* Live in-graph durations of pass one's two kernels: with timing on, the pass one of a
- * single-GPU one-graph solve (tpl_lanczos_two_pass with a device f, k >= 16) records HIP
- * events around k_p1_spmv and k_p1_axpy of 8 steps spread over the pass; this returns
- * their averages over the samples of the last timed solve (event to event: each includes
- * its launch's boundary, like pass2_spmv_us).                                     */
+/* Live durations of pass one's two kernels: with timing on, the pass one of a single-GPU
+ * two-pass solve with a device f (k >= 4) runs as four graphs with HIP events around the
+ * k_p1_spmv and the k_p1_axpy launch of its middle step (k / 2); this returns their
+ * averages over the timed solves since tpl_op_enable_timing (event to event: each
+ * includes its launch's boundary, like pass2_spmv_us), and the number of solves.  */
 tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_us,
                                int32_t* samples);
 

@@ -88,6 +88,9 @@ static tpl_status guarded(F&& f) {
     set_last_error("");
     return TPL_OK;
   } catch (const Error& e) {
+    // a failed HIP call leaves its status as the runtime's "last error", which the next
+    // launch's hipGetLastError() check would report as its own: clear it here
+    if (e.code == TPL_ERR_DEVICE || e.code == TPL_ERR_OUT_OF_MEMORY) (void)hipGetLastError();
     set_last_error(e.code, e.msg, e.det);
     return e.code;
   } catch (const std::bad_alloc&) {
@@ -127,13 +130,11 @@ enum GraphKind {
   kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
   kGPass1Elim = 7,    // (timed variant) pass one eliminating T_k's LU as it goes
   kGStandardElim = 8, // the standard pass eliminating T_k's LU as it goes (one-pass inv)
-  kGPass1Sampled = 9, // (timed variant) pass one with events around sampled steps' kernels
-  kGPass1ElimSampled = 10,
+  // (timed variant, tpl_op_step_samples) pass one in four graphs: the prologue and steps
+  // 1 .. js - 1, step js's k_p1_spmv alone, its k_p1_axpy alone, steps js + 1 .. k
+  // (+ 1: eliminating T_k's LU as it goes)
+  kGP1Head = 9, kGP1Spmv = 11, kGP1Axpy = 13, kGP1Tail = 15,
 };
-// Live in-graph timing of pass one's two kernels (tpl_op_step_samples): with timing on, a
-// single-GPU one-graph solve's pass one records events around k_p1_spmv and k_p1_axpy of
-// kStepSamples steps spread over the pass (step 1 + (2i + 1) k / (2 kStepSamples)).
-constexpr int kStepSamples = 8;
 // Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
 // run ahead of the host callback.
 constexpr int kCbBatchMax = 32;
@@ -243,9 +244,12 @@ struct tpl_op_s {
   size_t vext_cols = 0;
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
-  // sampled pass-one steps: [i][0] before k_p1_spmv, [1] between, [2] after k_p1_axpy
-  hipEvent_t sev[kStepSamples][3] = {};
-  int p1_samples = 0;               // samples recorded by the last timed solve
+  // live timing of pass one's kernels (tpl_op_step_samples): events before step js's
+  // k_p1_spmv, between it and its k_p1_axpy, after it; the sums over the timed solves
+  hipEvent_t sev[3] = {nullptr, nullptr, nullptr};
+  bool sev_pending = false;         // recorded by a solve, not yet added to the sums
+  double samp_spmv_ms = 0.0, samp_axpy_ms = 0.0;
+  int32_t p1_samples = 0;
   // tpl_plan_create: the host half of an operator only (rows, order, layout), for the
   // oracle's reduction order without a GPU; every device entry point refuses it
   bool plan_only = false;
@@ -674,15 +678,16 @@ void enqueue_p2_exchange(tpl_op_s* op, int j) {
 
 // Pass one, step j (k = requested steps). elim: also eliminate row j - 3 of T_k's LU
 // (the one-graph inv, k_p1_axpy).
-// sample >= 0: record the sample's events around the step's two kernels (single GPU).
+// part: 0 both kernels, 1 k_p1_spmv (and the exchange after it) only, 2 the rest only.
 void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false,
-                     int sample = -1) {
+                     int part = 0) {
   const CsrDev A = csr_dev(op, true);
-  if (sample >= 0) HIPCHK(hipEventRecord(op->sev[sample][0], op->stream));
+  if (part != 2) {
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
                          op->W, Vcol, j, op->stream));
-  if (sample >= 0) HIPCHK(hipEventRecord(op->sev[sample][1], op->stream));
   if (op->dist) enqueue_p1_exchange_a(op, A);
+  }
+  if (part == 1) return;
   if (op->hybrid)
     HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, op->dist->nranks, r_of(op, j),
                                j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol,
@@ -692,24 +697,14 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false
                      ? const_cast<double*>(op->S.Pb_r) + op->dist->rank : nullptr;
   HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k,
                          elim ? 1 : 0, op->stream, btot, btot ? op->d_bcnt : nullptr));
-  if (sample >= 0) HIPCHK(hipEventRecord(op->sev[sample][2], op->stream));
   if (op->dist && j < k) enqueue_p1_exchange_b(op, A, j);
 }
 
-// The sample index of step j of a k-step sampled pass one, or -1.
-int step_sample(int j, int k) {
-  if (k < 2 * kStepSamples) return -1;
-  for (int i = 0; i < kStepSamples; ++i)
-    if (j == 1 + (2 * i + 1) * k / (2 * kStepSamples)) return i;
-  return -1;
-}
-
-void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false,
-                   bool sampled = false) {
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false) {
   enqueue_p1_prologue(op);
   for (int j = 1; j <= (int)k; ++j) {
     double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
-    enqueue_p1_step(op, j, (int)k, Vcol, elim, sampled ? step_sample(j, (int)k) : -1);
+    enqueue_p1_step(op, j, (int)k, Vcol, elim);
     if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
   }
 }
@@ -851,7 +846,42 @@ HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
   return d;
 }
 
-// The whole two-pass solve as one graph (or, with live timing on, as three graphs with
+// Add the last sampled solve's two kernel times to the sums (its events have completed
+// once the solve returned: every solve ends with a stream synchronisation).
+void collect_samples(tpl_op_s* op) {
+  if (!op->sev_pending) return;
+  op->sev_pending = false;
+  HIPCHK(hipEventSynchronize(op->sev[2]));
+  float a = 0.f, b = 0.f;
+  HIPCHK(hipEventElapsedTime(&a, op->sev[0], op->sev[1]));
+  HIPCHK(hipEventElapsedTime(&b, op->sev[1], op->sev[2]));
+  op->samp_spmv_ms += a;
+  op->samp_axpy_ms += b;
+  op->p1_samples += 1;
+}
+
+// Live timing, single GPU: pass one as four graphs with HIP events around the two kernels
+// of its middle step js = k / 2 — event to event, each time includes its launch's
+// boundary, like pass two's per-launch figure. One sample per timed solve.
+void run_pass1_sampled(tpl_op_s* op, size_t k, bool elim) {
+  collect_samples(op);
+  const int js = (int)k / 2, ki = (int)k, e = elim ? 1 : 0;
+  run_graph(op, kGP1Head + e, k, [&] {
+    enqueue_p1_prologue(op);
+    for (int j = 1; j < js; ++j) enqueue_p1_step(op, j, ki, nullptr, elim);
+  });
+  HIPCHK(hipEventRecord(op->sev[0], op->stream));
+  run_graph(op, kGP1Spmv + e, k, [&] { enqueue_p1_step(op, js, ki, nullptr, elim, 1); });
+  HIPCHK(hipEventRecord(op->sev[1], op->stream));
+  run_graph(op, kGP1Axpy + e, k, [&] { enqueue_p1_step(op, js, ki, nullptr, elim, 2); });
+  HIPCHK(hipEventRecord(op->sev[2], op->stream));
+  op->sev_pending = true;
+  run_graph(op, kGP1Tail + e, k, [&] {
+    for (int j = js + 1; j <= ki; ++j) enqueue_p1_step(op, j, ki, nullptr, elim);
+  });
+}
+
+// The whole two-pass solve as one graph (or, with live timing on, as several graphs with
 // the events between them); no host round trip between the passes.
 void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
   const size_t key = 2 * k + (size_t)f;  // one graph per (k, f)
@@ -866,10 +896,10 @@ void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
     return;
   }
   HIPCHK(hipEventRecord(op->tev[0], op->stream));
-  const bool sampled = !op->dist && k >= 2 * kStepSamples;
-  run_graph(op, sampled ? (elim ? kGPass1ElimSampled : kGPass1Sampled) : (elim ? kGPass1Elim : kGPass1),
-            k, [&] { enqueue_pass1(op, k, false, false, elim, sampled); });
-  op->p1_samples = sampled ? kStepSamples : 0;
+  if (!op->dist && k >= 4)
+    run_pass1_sampled(op, k, elim);
+  else
+    run_graph(op, elim ? kGPass1Elim : kGPass1, k, [&] { enqueue_pass1(op, k, false, false, elim); });
   HIPCHK(hipEventRecord(op->tev[1], op->stream));
   run_graph(op, kGDevFtk, key, [&] { enqueue_ftk_dev(op, k, f); });
   HIPCHK(hipEventRecord(op->tev[2], op->stream));
@@ -990,8 +1020,7 @@ void init_op(tpl_op_s* op) {
   HIPCHK(hipEventCreate(&op->ev0));
   HIPCHK(hipEventCreate(&op->ev1));
   for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
-  for (auto& ev : op->sev)
-    for (hipEvent_t& e : ev) HIPCHK(hipEventCreate(&e));
+  for (hipEvent_t& e : op->sev) HIPCHK(hipEventCreate(&e));
 }
 
 // Contiguous blocks over items 0..m-1 with cost prefix[m+1]: cut where the prefix
@@ -1203,9 +1232,8 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     if (op->ev1) hipEventDestroy(op->ev1);
     for (hipEvent_t e : op->tev)
       if (e) hipEventDestroy(e);
-    for (auto& ev : op->sev)
-      for (hipEvent_t e : ev)
-        if (e) hipEventDestroy(e);
+    for (hipEvent_t e : op->sev)
+      if (e) hipEventDestroy(e);
     delete op;
   });
 }
@@ -1684,7 +1712,9 @@ tpl_status tpl_op_enable_timing(tpl_op_t op, int on) {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     op->timing = on != 0;
     op->p2_launches = 0;
+    op->sev_pending = false;
     op->p1_samples = 0;
+    op->samp_spmv_ms = op->samp_axpy_ms = 0.0;
   });
 }
 
@@ -1692,21 +1722,13 @@ tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_
                                int32_t* samples) {
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
+    set_device(op);
+    if (op->timing) collect_samples(op);
     if (!op->timing || op->p1_samples <= 0)
       fail(TPL_ERR_INVALID_ARGUMENT,
-           "no sampled solve (enable timing, then run a one-graph two-pass solve with k >= 16)");
-    set_device(op);
-    HIPCHK(hipEventSynchronize(op->tev[1]));
-    double s = 0.0, a = 0.0;
-    for (int i = 0; i < op->p1_samples; ++i) {
-      float t0 = 0.f, t1 = 0.f;
-      HIPCHK(hipEventElapsedTime(&t0, op->sev[i][0], op->sev[i][1]));
-      HIPCHK(hipEventElapsedTime(&t1, op->sev[i][1], op->sev[i][2]));
-      s += t0;
-      a += t1;
-    }
-    if (p1_spmv_us) *p1_spmv_us = 1000.0 * s / op->p1_samples;
-    if (p1_axpy_us) *p1_axpy_us = 1000.0 * a / op->p1_samples;
+           "no sampled solve (enable timing, then run a one-graph two-pass solve with k >= 4)");
+    if (p1_spmv_us) *p1_spmv_us = 1000.0 * op->samp_spmv_ms / op->p1_samples;
+    if (p1_axpy_us) *p1_axpy_us = 1000.0 * op->samp_axpy_ms / op->p1_samples;
     if (samples) *samples = op->p1_samples;
   });
 }
