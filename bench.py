@@ -265,7 +265,7 @@ def roofline_block(b_spmv, b_fused, p2_us, p1s_us, p1a_us, n_samp, steps, p1_ste
     if p1s_us:
         t1 = (p1_traffic or {}).get("k_p1_spmv")
         kern["k_p1_spmv"] = {"avg_launch_us_events": round(p1s_us, 3), "launches_per_solve": steps,
-                             "events": f"around step k/2's launch in each of the {n_samp} timed solves",
+                             "events": f"start-to-start, GPU real-time clock stamps of {n_samp} middle steps' launches in the last timed solve's pass-one graph",
                              "achieved": round(gbs(b_spmv, p1s_us), 1), "frac": frac(b_spmv, p1s_us),
                              "traffic": t1, "traffic_source": p1_traffic_src}
         kern["k_p1_axpy"] = {"avg_launch_us_events": round(p1a_us, 3), "launches_per_solve": steps,
@@ -521,7 +521,6 @@ def main():
         if dist is not None:
             dist.barrier()
 
-    op.enable_timing(True)  # resets the live sums: they cover the timed solves only
     barrier()
     stage_marker("timed_loop")
     t0 = time.perf_counter()
@@ -549,8 +548,8 @@ def main():
     b_fused = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
     achieved = b_spmv / (us * 1e-6) / 1e9
     p1_step_us = p1_us / steps_taken
-    # pass one's kernels, live: events around k_p1_spmv and k_p1_axpy of the middle step
-    # of every timed solve (single GPU, device f: pass one then runs as four graphs)
+    # pass one's kernels, live in the pass-one graph: start stamps (GPU real-time clock)
+    # of k_p1_spmv and k_p1_axpy on 8 consecutive middle steps of the last timed solve
     try:
         s1_us, a1_us, n_samp = op.step_samples()
     except Exception:  # noqa: BLE001 - partitioned / host f: no sampled pass one

@@ -206,10 +206,11 @@ tpl_status tpl_lanczos_two_pass(tpl_op_t op, const double* b, int64_t b_len, siz
                                 tpl_ftk_fn f, void* f_user, double* x_out, int mem);
 /* Where tpl_lanczos_two_pass evaluates the built-in f(T_k): mode 0 = host (two graphs
  * around the host call), 1 = device (the whole solve one graph), 2 = auto (default).
- *   inv: device for k <= 1365 (modes 1 and 2): the host solver's exact operations, its
- *        elimination done during pass one and its back substitution with correctly
- *        rounded (Markstein) divisions — bitwise the host result, never slower than the
- *        host round trip it removes.
+ *   inv: device for k <= 1365 in mode 1, k <= 500 in mode 2: the host solver's exact
+ *        operations, its elimination done during pass one and its back substitution with
+ *        correctly rounded (Markstein) divisions — bitwise the host result. Auto mode
+ *        stops at k = 500, the largest k measured no slower than the host round trip it
+ *        removes; at k = 1000-1365 the serial back substitution is slower.
  *   exp: device for k <= 1800 (modes 1 and 2): a Chebyshev expansion of exp over the
  *        Sturm-bracketed spectrum, parallel over the rows of T_k, within
  *        a small multiple of eps * exp(lambda_max) of the host QL result — the accuracy
@@ -335,11 +336,12 @@ tpl_status tpl_op_device_bytes(tpl_op_t op, uint64_t* bytes);
 tpl_status tpl_op_enable_timing(tpl_op_t op, int on);
 tpl_status tpl_op_pass_timing(tpl_op_t op, double* pass1_us, double* pass2_spmv_us,
                               int64_t* pass2_launches);
-/* Live durations of pass one's two kernels: with timing on, the pass one of a single-GPU
- * two-pass solve with a device f (k >= 4) runs as four graphs with HIP events around the
- * k_p1_spmv and the k_p1_axpy launch of its middle step (k / 2); this returns their
- * averages over the timed solves since tpl_op_enable_timing (event to event: each
- * includes its launch's boundary, like pass2_spmv_us), and the number of solves.  */
+/* Live in-graph durations of pass one's two kernels: with timing on, the pass-one graph
+ * of a single-GPU two-pass solve with a device f (k >= 11) has workgroup 0 of the
+ * k_p1_spmv and k_p1_axpy launches of 8 consecutive middle steps record its start on the
+ * GPU's 100 MHz real-time clock; this returns the average start-to-start interval of each
+ * kernel (its launch plus the boundary after it, like pass2_spmv_us) over those steps of
+ * the last timed solve, and the number of steps.                                   */
 tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_us,
                                int32_t* samples);
 

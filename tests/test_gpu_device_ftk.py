@@ -100,16 +100,24 @@ def test_device_inv_breakdown_no_op_launches():
 
 
 def test_auto_mode(kkt5k):
-    """Default (auto): one graph for the built-in inv up to k = 1365 (its LDS bound; round
-    4: never slower than the host path), the host solver between two graphs above."""
+    """Default (auto): one graph for the built-in inv up to k = 500 (round 5: the largest
+    k measured no slower than the host path, profiles/r05_ftk_timing.txt), the host solver
+    between two graphs above; mode 1 takes the device inv up to its LDS bound, 1365."""
     a = kkt5k.a
     op = HipCsrOp(a)
     b = std_rng_vector(a.shape[0])
-    for k in (128, 129, 500, 1365):
+    for k in (128, 129, 500):
         solvers.lanczos_two_pass(op, b, k, ftk.INV)
         assert op.flags() & ONE_GRAPH, k
+    for k in (501, 1365):
+        solvers.lanczos_two_pass(op, b, k, ftk.INV)
+        assert not op.flags() & ONE_GRAPH, k
+    op.set_device_ftk(1)
+    solvers.lanczos_two_pass(op, b, 1365, ftk.INV)
+    assert op.flags() & ONE_GRAPH
     solvers.lanczos_two_pass(op, b, 1366, ftk.INV)
     assert not op.flags() & ONE_GRAPH
+    op.set_device_ftk(2)
     solvers.lanczos_two_pass(op, b, 50, ftk.EXP)  # the built-in exp: on the device too
     assert op.flags() & ONE_GRAPH
     solvers.lanczos_two_pass(op, b, 50, lambda al, be: ftk.EXP(al, be))  # a host f stays
@@ -187,7 +195,7 @@ def test_one_pass_device_f(kkt5k):
         # relative_solution_deviation ~ 1e-16)
         xt = solvers.lanczos_two_pass(op, b, k, ftk.EXP)
         assert np.linalg.norm(xe - xt) <= 1e-13 * np.linalg.norm(xt), k
-    xd = solvers.lanczos(op, b, 500, ftk.INV)  # auto: the device inv up to k = 1365
+    xd = solvers.lanczos(op, b, 500, ftk.INV)  # auto: the device inv up to k = 500
     assert op.flags() & ONE_GRAPH
     op.set_device_ftk(False)
     assert same_bits_nan(xd, solvers.lanczos(op, b, 500, ftk.INV))

@@ -133,6 +133,13 @@ __device__ __forceinline__ void st_out(double* p, double v) {
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Live timing (tpl_op_step_samples): workgroup 0 records the launch's start on the
+// chip's 100 MHz real-time clock (a vector store; stamp is nullptr except in the sampled
+// launches of a timed solve).
+__device__ __forceinline__ void launch_stamp(unsigned long long* stamp) {
+  if (stamp && blockIdx.x == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
+}
+
 // Agent-scope load (global_load ... sc1): a value another XCD published write-through,
 // read past any stale copy in this XCD's L2.
 __device__ __forceinline__ double ld_agent(const double* p) {

@@ -170,8 +170,10 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 1)) void k_p1_spmv(CsrDev A, 
                                                   const double* __restrict__ r_cur,
                                                   const double* __restrict__ r_prev,
                                                   double* __restrict__ W,
-                                                  double* __restrict__ Vcol, int j) {
+                                                  double* __restrict__ Vcol, int j,
+                                                  unsigned long long* stamp) {
   TPL_MARK_FIRST();
+  launch_stamp(stamp);
   __shared__ double red[4], redb[4];
   extern __shared__ double lds[];
   p1_spmv_body<F, 1>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
@@ -184,7 +186,9 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 4)) void k_p1_spmv_wide(CsrDe
                                                   const double* __restrict__ r_cur,
                                                   const double* __restrict__ r_prev,
                                                   double* __restrict__ W,
-                                                  double* __restrict__ Vcol, int j) {
+                                                  double* __restrict__ Vcol, int j,
+                                                  unsigned long long* stamp) {
+  launch_stamp(stamp);
   __shared__ double red[4], redb[4];
   extern __shared__ double lds[];
   p1_spmv_body<F, 4>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
@@ -273,8 +277,10 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   const double* __restrict__ r_cur,
                                                   double* __restrict__ r_next, int j, int k,
                                                   int elim, double* __restrict__ tot,
-                                                  unsigned int* __restrict__ cnt) {
+                                                  unsigned int* __restrict__ cnt,
+                                                  unsigned long long* stamp) {
   __shared__ double red[4];
+  launch_stamp(stamp);
   if (elim && blockIdx.x == gridDim.x - 1) {
     if (threadIdx.x != 0 || j < 3) return;
     const int i = j - 3;
@@ -1340,35 +1346,37 @@ hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStrea
   return hipGetLastError();
 }
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
-                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s) {
+                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s,
+                   unsigned long long* stamp) {
   if (spmv_grid(A) <= 0) return hipGetLastError();
-  if (A.G2_r <= kTPB) return TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
-  return TPL_LAUNCH_CW(k_p1_spmv_wide, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j);
+  if (A.G2_r <= kTPB)
+    return TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp);
+  return TPL_LAUNCH_CW(k_p1_spmv_wide, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp);
   return hipGetLastError();
 }
 template <bool FOLD>
 static void p1_axpy_np(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                        double* r_next, int j, int k, int elim, double* tot, unsigned int* cnt,
-                       dim3 g, hipStream_t s) {
+                       unsigned long long* st, dim3 g, hipStream_t s) {
   const dim3 b(kTPB);
   if (A.NA_r <= 2 * kTPB)
-    hipLaunchKernelGGL((k_p1_axpy<2, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt);
+    hipLaunchKernelGGL((k_p1_axpy<2, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
   else if (A.NA_r <= 4 * kTPB)
-    hipLaunchKernelGGL((k_p1_axpy<4, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt);
+    hipLaunchKernelGGL((k_p1_axpy<4, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
   else if (A.NA_r <= 8 * kTPB)
-    hipLaunchKernelGGL((k_p1_axpy<8, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt);
+    hipLaunchKernelGGL((k_p1_axpy<8, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
   else
-    hipLaunchKernelGGL((k_p1_axpy<12, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt);
+    hipLaunchKernelGGL((k_p1_axpy<12, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
 }
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, int elim, hipStream_t s, double* tot,
-                   unsigned int* cnt) {
+                   unsigned int* cnt, unsigned long long* stamp) {
   const dim3 g(g2_grid(A) + (elim ? 1 : 0));
   if (tot) {
     if (A.G2 > 4 * kTPB || !cnt || elim) return hipErrorInvalidValue;
-    p1_axpy_np<true>(A, S, W, r_cur, r_next, j, k, elim, tot, cnt, g, s);
+    p1_axpy_np<true>(A, S, W, r_cur, r_next, j, k, elim, tot, cnt, stamp, g, s);
   } else {
-    p1_axpy_np<false>(A, S, W, r_cur, r_next, j, k, elim, nullptr, nullptr, g, s);
+    p1_axpy_np<false>(A, S, W, r_cur, r_next, j, k, elim, nullptr, nullptr, stamp, g, s);
   }
   return hipGetLastError();
 }

@@ -34,14 +34,16 @@ namespace tpl {
 namespace launch {
 hipError_t spmv(const CsrDev& A, const double* x, double* y, hipStream_t s);
 hipError_t p1_init(const CsrDev& A, const DevState& S, const double* b, hipStream_t s);
+// stamp: workgroup 0 records the launch's start there (live timing), or nullptr
 hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const double* r_cur,
-                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s);
+                   const double* r_prev, double* W, double* Vcol, int j, hipStream_t s,
+                   unsigned long long* stamp = nullptr);
 // elim: one more workgroup eliminates row j - 3 of T_k's LU (one-graph inv)
 // tot != nullptr (replicated partition): the last workgroup also reduces the G2 norm
 // partials into *tot, this rank's beta total (cnt: its arrival counter, zero between launches)
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
                    double* r_next, int j, int k, int elim, hipStream_t s, double* tot = nullptr,
-                   unsigned int* cnt = nullptr);
+                   unsigned int* cnt = nullptr, unsigned long long* stamp = nullptr);
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
 hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
                    const int32_t* idx, hipStream_t s);
@@ -130,25 +132,30 @@ enum GraphKind {
   kGPass2Dyn = 6,     // (timed variant) the k - 1 step launches of a one-graph solve
   kGPass1Elim = 7,    // (timed variant) pass one eliminating T_k's LU as it goes
   kGStandardElim = 8, // the standard pass eliminating T_k's LU as it goes (one-pass inv)
-  // (timed variant, tpl_op_step_samples) pass one in four graphs: the prologue and steps
-  // 1 .. js - 1, step js's k_p1_spmv alone, its k_p1_axpy alone, steps js + 1 .. k
-  // (+ 1: eliminating T_k's LU as it goes)
-  kGP1Head = 9, kGP1Spmv = 11, kGP1Axpy = 13, kGP1Tail = 15,
+  kGPass1Stamped = 9, // (timed variant) pass one with start stamps on kStampSteps steps
+  kGPass1ElimStamped = 10,
 };
+// Live timing of pass one's kernels (tpl_op_step_samples): in a timed solve, workgroup 0
+// of the k_p1_spmv and k_p1_axpy launches of kStampSteps consecutive middle steps (and of
+// the next step's k_p1_spmv) records its start on the 100 MHz real-time clock; a kernel's
+// launch time is the start-to-start interval, boundary included (as pass two's figure).
+constexpr int kStampSteps = 8;
 // Callback polling (tpl_lanczos_standard with a step callback): largest batch of steps
 // run ahead of the host callback.
 constexpr int kCbBatchMax = 32;
 // One-graph solves keep the device f(T_k)'s working rows in LDS (k_ftk_inv: 11 k doubles,
 // 120 KB at this k; gfx950 has 160 KiB of LDS per workgroup).
 constexpr size_t kDevFtkMaxK = 1365;
-// Auto mode: the device inv at every k it holds. Its elimination runs during pass one
-// (k_p1_axpy's extra workgroup) and its back substitution with Markstein divisions, so
-// the one-graph solve is never slower than the host round trip it replaces (round 4, same
-// box, profiles/r04_ftk_timing.txt: 0.574 vs 0.583 ms at 5k arcs k = 50, 2.390 vs 2.412
-// at 50k k = 200, 9.312 vs 9.315 ms at the 500k headline k = 500; round 3, with the
-// whole elimination after pass one and IEEE divisions, the device chain alone took 130 us
-// at k = 500 and auto mode stopped at k = 128).
-constexpr size_t kDevFtkAutoK = kDevFtkMaxK;
+// Auto mode: the device inv up to k = 500, the largest k at which it was measured no
+// slower than the host round trip it replaces. Its elimination runs during pass one
+// (k_p1_axpy's extra workgroup) and its back substitution with Markstein divisions (round
+// 4, same box, profiles/r04_ftk_timing.txt: 0.574 vs 0.583 ms at 5k arcs k = 50, 2.390 vs
+// 2.412 at 50k k = 200, 9.312 vs 9.315 ms at the 500k headline k = 500); past that the
+// serial back substitution grows longer than the round trip (round 5, same box,
+// profiles/r05_ftk_timing.txt: 10.36 vs 10.24 ms at 5k arcs k = 1000, 14.16 vs 13.84 at
+// k = 1365; 11.18 vs 10.99 and 15.62 vs 15.05 ms at 50k arcs). Mode 1 still takes the
+// device inv up to kDevFtkMaxK.
+constexpr size_t kDevFtkAutoK = 500;
 // The device exp (k_ftk_exp, a Chebyshev expansion: parallel over the rows of T_k) keeps
 // 4 k + 4 doubles of dynamic LDS plus 8.2 KB of static arrays: 65.8 KB at this k, which
 // gfx950's 160 KiB of LDS per workgroup holds (a 64 KiB part would need k <= 1790).
@@ -244,11 +251,9 @@ struct tpl_op_s {
   size_t vext_cols = 0;
   hipEvent_t tev[4] = {nullptr, nullptr, nullptr, nullptr};
   int64_t p2_launches = 0;
-  // live timing of pass one's kernels (tpl_op_step_samples): events before step js's
-  // k_p1_spmv, between it and its k_p1_axpy, after it; the sums over the timed solves
-  hipEvent_t sev[3] = {nullptr, nullptr, nullptr};
-  bool sev_pending = false;         // recorded by a solve, not yet added to the sums
-  double samp_spmv_ms = 0.0, samp_axpy_ms = 0.0;
+  // live timing of pass one's kernels: start stamps of the last timed solve's sampled
+  // launches (2 kStampSteps + 1), tpl_op_step_samples
+  unsigned long long* d_stamps = nullptr;
   int32_t p1_samples = 0;
   // tpl_plan_create: the host half of an operator only (rows, order, layout), for the
   // oracle's reduction order without a GPU; every device entry point refuses it
@@ -678,16 +683,13 @@ void enqueue_p2_exchange(tpl_op_s* op, int j) {
 
 // Pass one, step j (k = requested steps). elim: also eliminate row j - 3 of T_k's LU
 // (the one-graph inv, k_p1_axpy).
-// part: 0 both kernels, 1 k_p1_spmv (and the exchange after it) only, 2 the rest only.
+// st1 / st2: start stamps of the step's k_p1_spmv / k_p1_axpy launch (live timing), or nullptr.
 void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false,
-                     int part = 0) {
+                     unsigned long long* st1 = nullptr, unsigned long long* st2 = nullptr) {
   const CsrDev A = csr_dev(op, true);
-  if (part != 2) {
   HIPCHK(launch::p1_spmv(A, op->S, rG_of(op, j), r_of(op, j), j >= 2 ? r_of(op, j - 1) : nullptr,
-                         op->W, Vcol, j, op->stream));
+                         op->W, Vcol, j, op->stream, st1));
   if (op->dist) enqueue_p1_exchange_a(op, A);
-  }
-  if (part == 1) return;
   if (op->hybrid)
     HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, op->dist->nranks, r_of(op, j),
                                j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol,
@@ -696,15 +698,26 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false
   double* btot = (beta_folded(op, A) && j < k)
                      ? const_cast<double*>(op->S.Pb_r) + op->dist->rank : nullptr;
   HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k,
-                         elim ? 1 : 0, op->stream, btot, btot ? op->d_bcnt : nullptr));
+                         elim ? 1 : 0, op->stream, btot, btot ? op->d_bcnt : nullptr, st2));
   if (op->dist && j < k) enqueue_p1_exchange_b(op, A, j);
 }
 
-void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false) {
+// First stamped step of a k-step pass one (steps js .. js + kStampSteps - 1, and the
+// k_p1_spmv of the step after), or 0: the pass is too short to sample.
+int stamp_first(size_t k) {
+  return k >= (size_t)kStampSteps + 3 ? (int)(k - kStampSteps) / 2 + 1 : 0;
+}
+
+void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = false,
+                   bool stamped = false) {
   enqueue_p1_prologue(op);
+  const int js = stamped ? stamp_first(k) : 0;
   for (int j = 1; j <= (int)k; ++j) {
     double* Vcol = storeV ? op->d_V + (size_t)(j - 1) * op->n : nullptr;
-    enqueue_p1_step(op, j, (int)k, Vcol, elim);
+    const int i = j - js;  // stamp slots: spmv of step js + i at 2i, its axpy at 2i + 1
+    unsigned long long* st1 = js && i >= 0 && i <= kStampSteps ? op->d_stamps + 2 * i : nullptr;
+    unsigned long long* st2 = js && i >= 0 && i < kStampSteps ? op->d_stamps + 2 * i + 1 : nullptr;
+    enqueue_p1_step(op, j, (int)k, Vcol, elim, st1, st2);
     if (reorth && j < (int)k) enqueue_reorth(op, j, reorth);
   }
 }
@@ -846,41 +859,6 @@ HostDecomp fetch_decomp(tpl_op_s* op, size_t k) {
   return d;
 }
 
-// Add the last sampled solve's two kernel times to the sums (its events have completed
-// once the solve returned: every solve ends with a stream synchronisation).
-void collect_samples(tpl_op_s* op) {
-  if (!op->sev_pending) return;
-  op->sev_pending = false;
-  HIPCHK(hipEventSynchronize(op->sev[2]));
-  float a = 0.f, b = 0.f;
-  HIPCHK(hipEventElapsedTime(&a, op->sev[0], op->sev[1]));
-  HIPCHK(hipEventElapsedTime(&b, op->sev[1], op->sev[2]));
-  op->samp_spmv_ms += a;
-  op->samp_axpy_ms += b;
-  op->p1_samples += 1;
-}
-
-// Live timing, single GPU: pass one as four graphs with HIP events around the two kernels
-// of its middle step js = k / 2 — event to event, each time includes its launch's
-// boundary, like pass two's per-launch figure. One sample per timed solve.
-void run_pass1_sampled(tpl_op_s* op, size_t k, bool elim) {
-  collect_samples(op);
-  const int js = (int)k / 2, ki = (int)k, e = elim ? 1 : 0;
-  run_graph(op, kGP1Head + e, k, [&] {
-    enqueue_p1_prologue(op);
-    for (int j = 1; j < js; ++j) enqueue_p1_step(op, j, ki, nullptr, elim);
-  });
-  HIPCHK(hipEventRecord(op->sev[0], op->stream));
-  run_graph(op, kGP1Spmv + e, k, [&] { enqueue_p1_step(op, js, ki, nullptr, elim, 1); });
-  HIPCHK(hipEventRecord(op->sev[1], op->stream));
-  run_graph(op, kGP1Axpy + e, k, [&] { enqueue_p1_step(op, js, ki, nullptr, elim, 2); });
-  HIPCHK(hipEventRecord(op->sev[2], op->stream));
-  op->sev_pending = true;
-  run_graph(op, kGP1Tail + e, k, [&] {
-    for (int j = js + 1; j <= ki; ++j) enqueue_p1_step(op, j, ki, nullptr, elim);
-  });
-}
-
 // The whole two-pass solve as one graph (or, with live timing on, as several graphs with
 // the events between them); no host round trip between the passes.
 void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
@@ -896,10 +874,14 @@ void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
     return;
   }
   HIPCHK(hipEventRecord(op->tev[0], op->stream));
-  if (!op->dist && k >= 4)
-    run_pass1_sampled(op, k, elim);
-  else
-    run_graph(op, elim ? kGPass1Elim : kGPass1, k, [&] { enqueue_pass1(op, k, false, false, elim); });
+  const bool stamped = !op->dist && stamp_first(k) > 0;
+  if (stamped && !op->d_stamps) {
+    dev_alloc(op, &op->d_stamps, 32 * sizeof(unsigned long long));
+    HIPCHK(hipMemset(op->d_stamps, 0, 32 * sizeof(unsigned long long)));
+  }
+  run_graph(op, stamped ? (elim ? kGPass1ElimStamped : kGPass1Stamped) : (elim ? kGPass1Elim : kGPass1),
+            k, [&] { enqueue_pass1(op, k, false, false, elim, stamped); });
+  op->p1_samples = stamped ? kStampSteps : 0;
   HIPCHK(hipEventRecord(op->tev[1], op->stream));
   run_graph(op, kGDevFtk, key, [&] { enqueue_ftk_dev(op, k, f); });
   HIPCHK(hipEventRecord(op->tev[2], op->stream));
@@ -1020,7 +1002,6 @@ void init_op(tpl_op_s* op) {
   HIPCHK(hipEventCreate(&op->ev0));
   HIPCHK(hipEventCreate(&op->ev1));
   for (hipEvent_t& e : op->tev) HIPCHK(hipEventCreate(&e));
-  for (hipEvent_t& e : op->sev) HIPCHK(hipEventCreate(&e));
 }
 
 // Contiguous blocks over items 0..m-1 with cost prefix[m+1]: cut where the prefix
@@ -1231,8 +1212,6 @@ tpl_status tpl_op_destroy(tpl_op_t op) {
     if (op->ev0) hipEventDestroy(op->ev0);
     if (op->ev1) hipEventDestroy(op->ev1);
     for (hipEvent_t e : op->tev)
-      if (e) hipEventDestroy(e);
-    for (hipEvent_t e : op->sev)
       if (e) hipEventDestroy(e);
     delete op;
   });
@@ -1712,9 +1691,7 @@ tpl_status tpl_op_enable_timing(tpl_op_t op, int on) {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     op->timing = on != 0;
     op->p2_launches = 0;
-    op->sev_pending = false;
     op->p1_samples = 0;
-    op->samp_spmv_ms = op->samp_axpy_ms = 0.0;
   });
 }
 
@@ -1723,13 +1700,20 @@ tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_
   return guarded([&] {
     if (!op) fail(TPL_ERR_INVALID_ARGUMENT, "op is NULL");
     set_device(op);
-    if (op->timing) collect_samples(op);
-    if (!op->timing || op->p1_samples <= 0)
+    if (!op->timing || op->p1_samples <= 0 || !op->d_stamps)
       fail(TPL_ERR_INVALID_ARGUMENT,
-           "no sampled solve (enable timing, then run a one-graph two-pass solve with k >= 4)");
-    if (p1_spmv_us) *p1_spmv_us = 1000.0 * op->samp_spmv_ms / op->p1_samples;
-    if (p1_axpy_us) *p1_axpy_us = 1000.0 * op->samp_axpy_ms / op->p1_samples;
-    if (samples) *samples = op->p1_samples;
+           "no sampled solve (enable timing, then run a two-pass solve with a device f, k >= 11)");
+    unsigned long long t[2 * kStampSteps + 1];
+    HIPCHK(hipMemcpyAsync(t, op->d_stamps, sizeof(t), hipMemcpyDeviceToHost, op->stream));
+    sync_checked(op);
+    double s1 = 0.0, s2 = 0.0;  // 100 MHz ticks
+    for (int i = 0; i < kStampSteps; ++i) {
+      s1 += (double)(t[2 * i + 1] - t[2 * i]);
+      s2 += (double)(t[2 * i + 2] - t[2 * i + 1]);
+    }
+    if (p1_spmv_us) *p1_spmv_us = 0.01 * s1 / kStampSteps;
+    if (p1_axpy_us) *p1_axpy_us = 0.01 * s2 / kStampSteps;
+    if (samples) *samples = kStampSteps;
   });
 }
 
