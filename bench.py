@@ -330,6 +330,32 @@ def predicted_block(world: int, k: int, steps: int, solve_s: float):
             "implied_L_us": round((1000.0 * solve_s - t0) * 1000.0 / c, 2)}
 
 
+def predicted_curve(k: int, single_ms: float):
+    """predicted_block's model for N = 2, 4, 8 at a few all-gather latencies L: ms per
+    solve and the speed-up over the one-GPU solve measured in this run."""
+    try:
+        with open(RANK_SHARE_FILE) as f:
+            rs = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if rs.get("k") != k:
+        return None
+    out = {"source": "profiles/rank_share.json (scripts/rank_share.py): rank 0's share of the "
+                     "replicated partition through one RCCL rank + (3k - 1) all-gathers of "
+                     "latency L", "one_gpu_ms": round(single_ms, 3), "N": {}}
+    for n in ("2", "4", "8"):
+        sh = rs.get("shares", {}).get(n)
+        if not sh:
+            continue
+        t0 = sh["one_rank_replicated"]["ms_per_solve"]
+        c = sh["collectives_per_solve"]
+        out["N"][n] = {"ms_1rank_share": t0, "kernels_only_speedup": round(single_ms / t0, 2),
+                       **{f"L{L}us": {"ms": round(t0 + c * L / 1000.0, 2),
+                                      "speedup": round(single_ms / (t0 + c * L / 1000.0), 2)}
+                          for L in (5, 10, 20)}}
+    return out
+
+
 # ---- N > 1: the parent process (never touches the GPU) ------------------------------
 def stage_marker(stage: str) -> None:
     """Append this rank's progress to its marker file (TPL_BENCH_STAGE_DIR, set by the
@@ -833,6 +859,11 @@ def main():
             "k_p2_spmv_us": round(u5, 3),
             "frac": round(op5.algo_bytes(_lib.TPL_KERNEL_SPMV) / (u5 * 1e-6) / 1e9 / HBM_PEAK_GBS, 4)}
         op5.close()
+        # the 1 -> 8 curve the driver's node would measure, predicted from the committed
+        # per-rank shares (scripts/rank_share.py) against this GPU's one-GPU solve
+        curve = predicted_curve(args.k, 1000.0 * d5)
+        if curve is not None:
+            out["configs4_5m_1gpu"]["predicted_scaling"] = curve
     if rank == 0 and args.cpu_baseline and world == 1 and not partitioned:
         import oracle  # CPU baseline only (reference-order restatement, single thread)
         from oracle import ftk_ref

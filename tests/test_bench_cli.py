@@ -143,3 +143,35 @@ def test_parent_never_kills_a_reused_pid(tmp_path, capsys, monkeypatch):
     finally:
         sleeper.kill()
         sleeper.wait()
+
+
+def test_prediction_and_roofline_blocks(tmp_path, monkeypatch):
+    """The N > 1 line's `predicted` block and the N = 1 line's predicted curve come from
+    the committed rank shares with the stated model (ms_1rank + (3k - 1) L); the roofline
+    names the kernel with the larger live time share and carries both SpMVs."""
+    rs = {"k": 500, "shares": {"8": {"rank0_rows": 10, "rank0_nnz": 20,
+                                     "one_rank_replicated": {"ms_per_solve": 15.0, "steps": 500,
+                                                             "pass1_us_per_step": 20.0,
+                                                             "pass2_us_per_step": 10.0},
+                                     "single_gpu": {"ms_per_solve": 11.0},
+                                     "collectives_per_step": {"pass1": 2, "pass2": 1},
+                                     "collectives_per_solve": 1499}}}
+    f = tmp_path / "rank_share.json"
+    f.write_text(json.dumps(rs))
+    monkeypatch.setattr(bench, "RANK_SHARE_FILE", str(f))
+    p = bench.predicted_block(8, 500, 500, 0.030)
+    assert p["ms_at_L_us"]["10"] == round(15.0 + 14.99, 3)
+    assert p["implied_L_us"] == round((30.0 - 15.0) * 1000.0 / 1499, 2)
+    assert bench.predicted_block(4, 500, 500, 0.03) is None  # no share for N = 4
+    assert "error" in bench.predicted_block(8, 400, 400, 0.03)
+    c = bench.predicted_curve(500, 66.0)
+    assert c["N"]["8"]["L10us"]["speedup"] == round(66.0 / (15.0 + 14.99), 2)
+    r = bench.roofline_block(34e6, 40e6, 6.3, 6.5, 4.6, 8, 500, 11.1, 8.8e-3, 22e6, "p2",
+                             {"k_p1_spmv": 19e6, "k_p1_axpy": 12e6}, "p1", {}, False)
+    assert r["kernel"] == "k_p1_spmv" and r["avg_launch_us_events"] == 6.5
+    assert r["frac"] == round(34e6 / 6.5e-6 / 1e9 / 8000.0, 4)
+    assert r["frac_counter_bytes"] == round(19e6 / 6.5e-6 / 1e9 / 8000.0, 4)
+    assert set(r["kernels"]) == {"k_p1_spmv", "k_p2_spmv", "k_p1_axpy"}
+    r2 = bench.roofline_block(34e6, 40e6, 6.3, None, None, 0, 500, 11.1, 8.8e-3, None, None,
+                              None, None, {}, True)
+    assert r2["kernel"].startswith("k_p2_spmv") and "all_spmv_time_weighted_frac" not in r2
