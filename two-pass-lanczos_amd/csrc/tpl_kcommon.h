@@ -140,13 +140,6 @@ __device__ __forceinline__ void launch_stamp(unsigned long long* stamp) {
   if (stamp && blockIdx.x == 0 && threadIdx.x == 0) *stamp = __builtin_amdgcn_s_memrealtime();
 }
 
-// Agent-scope load (global_load ... sc1): a value another XCD published write-through,
-// read past any stale copy in this XCD's L2.
-__device__ __forceinline__ double ld_agent(const double* p) {
-  return __longlong_as_double((long long)__hip_atomic_load(
-      reinterpret_cast<const unsigned long long*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-
 // Pins a value as computed unconditionally: without it the compiler sinks the loads
 // feeding a product used under a select (padding entries) into a branch, where they
 // issue late behind an s_waitcnt vmcnt(0) and serialise the workgroup's round trips.

@@ -264,21 +264,12 @@ __device__ __forceinline__ double div_rn(double a, double b, double y, bool b_ok
 // (lu_row): its inputs beta_{j-3}, alpha_{j-2} and beta_{j-2} (0-based) are all known
 // once this step's k_p1_spmv has reduced beta — the row is done off the critical path,
 // so only the last rows and the back substitution remain after pass one (k_ftk_inv).
-// FOLD (replicated-long-row partition): the workgroup that stores the last of the G2
-// norm partials also reduces them to this rank's beta total (*tot, the slot the
-// all-gather sends) — the tree the separate rank-total launch (k_reorth_reduce) applied,
-// so the bits are the same, one launch per pass-one step fewer (round 5). The arrival
-// hand-off is the SpMV bins' (publish write-through, drain, ONE agent-scope atomic add;
-// the add that returns G2 - 1 is the last), with the counter reset by that last arriver
-// (every launch that stores partials arrives G2 times; a stopped or final step none).
-template <int NP, bool FOLD>
+template <int NP>
 __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   const double* __restrict__ W,
                                                   const double* __restrict__ r_cur,
                                                   double* __restrict__ r_next, int j, int k,
-                                                  int elim, double* __restrict__ tot,
-                                                  unsigned int* __restrict__ cnt,
-                                                  unsigned long long* stamp) {
+                                                  int elim, unsigned long long* stamp) {
   __shared__ double red[4];
   launch_stamp(stamp);
   if (elim && blockIdx.x == gridDim.x - 1) {
@@ -375,35 +366,8 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
          *reinterpret_cast<const double2*>(r_cur + i0));
   TPL_MARK_AT(kAxpyMarkBase, 3);
   const double p = block_sum_tail(acc, red);
-  if constexpr (!FOLD) {
-    if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
-    TPL_MARK_AT(kAxpyMarkBase, 5);
-  } else {
-    __shared__ int last;
-    if (threadIdx.x == 0) {
-      st_out(S.Pb + rb, p);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const unsigned int arrived =
-          __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      last = arrived == (unsigned int)(A.G2 - 1);
-    }
-    __syncthreads();  // also: every lane has read block_sum_tail's LDS words
-    if (!last) return;
-    // every partial was drained before its writer's add, and this workgroup's loads
-    // follow its own (the last) add: agent-scope loads, past any stale L2 line
-    PartialRegs<4> pr;  // G2 <= 1024 (tpl_op_set_schedule's max_g2)
-#pragma unroll
-    for (int u = 0; u < 4; ++u) pr.v[u] = ld_agent(S.Pb + clampi(threadIdx.x + u * kTPB, A.G2 - 1));
-    double s = 0.0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u)
-      if ((int)threadIdx.x + u * kTPB < A.G2) s = s + pr.v[u];
-    const double t = block_sum(s, red);  // finish_partials' order: s += P[t + 256q], tree256
-    if (threadIdx.x == 0) {
-      *tot = t;
-      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  if (threadIdx.x == 0) S.Pb[rb] = p;  // plain: write-through measured +0.35 us here
+  TPL_MARK_AT(kAxpyMarkBase, 5);
 }
 
 // Pass two prologue: v_1 = b * (1/||b||); x = v_1 * y_1 (src/algorithms/lanczos_two_pass.rs:248-252).
@@ -1354,30 +1318,18 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
   return TPL_LAUNCH_CW(k_p1_spmv_wide, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp);
   return hipGetLastError();
 }
-template <bool FOLD>
-static void p1_axpy_np(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
-                       double* r_next, int j, int k, int elim, double* tot, unsigned int* cnt,
-                       unsigned long long* st, dim3 g, hipStream_t s) {
-  const dim3 b(kTPB);
-  if (A.NA_r <= 2 * kTPB)
-    hipLaunchKernelGGL((k_p1_axpy<2, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
-  else if (A.NA_r <= 4 * kTPB)
-    hipLaunchKernelGGL((k_p1_axpy<4, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
-  else if (A.NA_r <= 8 * kTPB)
-    hipLaunchKernelGGL((k_p1_axpy<8, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
-  else
-    hipLaunchKernelGGL((k_p1_axpy<12, FOLD>), g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, tot, cnt, st);
-}
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
-                   double* r_next, int j, int k, int elim, hipStream_t s, double* tot,
-                   unsigned int* cnt, unsigned long long* stamp) {
-  const dim3 g(g2_grid(A) + (elim ? 1 : 0));
-  if (tot) {
-    if (A.G2 > 4 * kTPB || !cnt || elim) return hipErrorInvalidValue;
-    p1_axpy_np<true>(A, S, W, r_cur, r_next, j, k, elim, tot, cnt, stamp, g, s);
-  } else {
-    p1_axpy_np<false>(A, S, W, r_cur, r_next, j, k, elim, nullptr, nullptr, stamp, g, s);
-  }
+                   double* r_next, int j, int k, int elim, hipStream_t s,
+                   unsigned long long* st) {
+  const dim3 g(g2_grid(A) + (elim ? 1 : 0)), b(kTPB);
+  if (A.NA_r <= 2 * kTPB)
+    hipLaunchKernelGGL(k_p1_axpy<2>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, st);
+  else if (A.NA_r <= 4 * kTPB)
+    hipLaunchKernelGGL(k_p1_axpy<4>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, st);
+  else if (A.NA_r <= 8 * kTPB)
+    hipLaunchKernelGGL(k_p1_axpy<8>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, st);
+  else
+    hipLaunchKernelGGL(k_p1_axpy<12>, g, b, 0, s, A, S, W, r_cur, r_next, j, k, elim, st);
   return hipGetLastError();
 }
 hipError_t p2_init(int64_t n, const DevState& S, const double* b, double* v1, double* x,

@@ -39,11 +39,9 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s,
                    unsigned long long* stamp = nullptr);
 // elim: one more workgroup eliminates row j - 3 of T_k's LU (one-graph inv)
-// tot != nullptr (replicated partition): the last workgroup also reduces the G2 norm
-// partials into *tot, this rank's beta total (cnt: its arrival counter, zero between launches)
 hipError_t p1_axpy(const CsrDev& A, const DevState& S, const double* W, const double* r_cur,
-                   double* r_next, int j, int k, int elim, hipStream_t s, double* tot = nullptr,
-                   unsigned int* cnt = nullptr, unsigned long long* stamp = nullptr);
+                   double* r_next, int j, int k, int elim, hipStream_t s,
+                   unsigned long long* stamp = nullptr);
 hipError_t p2_tail(int64_t n, const DevState& S, double* x, double* const V[3], hipStream_t s);
 hipError_t permute(int64_t n, int cols, double* out, int64_t ldo, const double* in, int64_t ldi,
                    const int32_t* idx, hipStream_t s);
@@ -219,8 +217,6 @@ struct tpl_op_s {
   double *bG = nullptr, *RG[3] = {nullptr, nullptr, nullptr}, *V2G[3] = {nullptr, nullptr, nullptr},
          *tmpG = nullptr;
   double* d_rsum = nullptr;         // [nranks alpha totals][nranks norm totals] (partition)
-  unsigned int* d_bcnt = nullptr;   // k_p1_axpy's arrival counter (replicated partition: the
-                                    // beta rank total folded into it), its own 128-B line
   // solver state
   size_t kcap = 0;
   void* d_state = nullptr;  // flags | norms | alphas | betas | y | Pa | Pb | Pr
@@ -653,14 +649,11 @@ void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
     dist_allgather(op, op->d_rsum, 1);
   }
 }
-// Replicated partition: k_p1_axpy's last workgroup reduces the rank's beta total (its
-// register tree holds up to 1024 partials, the default max_g2); else a separate launch.
-bool beta_folded(const tpl_op_s* op, const CsrDev& A) { return op->hybrid && A.G2 <= 1024; }
-
 void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
   if (op->hybrid) {
-    if (!beta_folded(op, A))
-      dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+    // the rank's beta total: its own one-workgroup launch (folding it into k_p1_axpy's
+    // last arriver measured slower, round 5: DESIGN.md §6.3)
+    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
     dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
   } else {
     const int R = op->dist->nranks;
@@ -694,11 +687,8 @@ void enqueue_p1_step(tpl_op_s* op, int j, int k, double* Vcol, bool elim = false
     HIPCHK(launch::long_epi_p1(A, op->S, op->d_yall, op->dist->nranks, r_of(op, j),
                                j >= 2 ? r_of(op, j - 1) : nullptr, op->W, Vcol,
                                op->d_rsum + op->dist->nranks, j, op->stream));
-  // replicated partition: the beta rank total is reduced by k_p1_axpy's last workgroup
-  double* btot = (beta_folded(op, A) && j < k)
-                     ? const_cast<double*>(op->S.Pb_r) + op->dist->rank : nullptr;
   HIPCHK(launch::p1_axpy(A, op->S, op->W, r_of(op, j), op->R[(j + 1) % 3], j, k,
-                         elim ? 1 : 0, op->stream, btot, btot ? op->d_bcnt : nullptr, st2));
+                         elim ? 1 : 0, op->stream, st2));
   if (op->dist && j < k) enqueue_p1_exchange_b(op, A, j);
 }
 
@@ -980,10 +970,8 @@ void init_op(tpl_op_s* op) {
     // [nranks alpha totals | long-row alpha partials (hybrid) | nranks norm totals]
     const size_t nr = (size_t)op->dist->nranks;
     const size_t cnt = 2 * nr + (op->hybrid ? (size_t)long_epi_blocks(op) : 0);
-    const size_t cnt_pad = (cnt + 15) / 16 * 16;  // the arrival counter on a 128-B line
-    dev_alloc(op, &op->d_rsum, (cnt_pad + 16) * sizeof(double));
-    HIPCHK(hipMemset(op->d_rsum, 0, (cnt_pad + 16) * sizeof(double)));
-    op->d_bcnt = reinterpret_cast<unsigned int*>(op->d_rsum + cnt_pad);
+    dev_alloc(op, &op->d_rsum, cnt * sizeof(double));
+    HIPCHK(hipMemset(op->d_rsum, 0, cnt * sizeof(double)));
     if (op->hybrid) {
       // every rank's chunk count (each rank's short rows are a contiguous block of the
       // global split, chunked by kChunkRows: every rank computes all counts alike)
