@@ -104,6 +104,11 @@ def parse(argv=None):
     p.add_argument("--pcie", type=int, default=1, help="N=1: also time host b / x (PCIe)")
     p.add_argument("--parity", type=int, default=1,
                    help="0 to skip the parity block (digests vs tests/golden/parity.json)")
+    p.add_argument("--replicas", type=int, default=1,
+                   help="N > 1: `value` is the headline solve run independently on every GPU "
+                        "(weak scaling, no collective); the row-partitioned configs[4] solve "
+                        "follows in the same run as `partitioned_configs4`. 0: `value` is the "
+                        "partitioned solve itself")
     p.add_argument("--dist-mode", choices=("auto", "replicated", "rows"), default="auto",
                    help="partition of the N > 1 solve: replicated long rows (auto: when the "
                         "matrix allows it) or row blocks with the whole vector all-gathered")
@@ -356,6 +361,125 @@ def predicted_curve(k: int, single_ms: float):
     return out
 
 
+def run_replicas(args, rank: int, world: int, dist, device: int) -> dict:
+    """N > 1, `value`: the headline workload (BASELINE configs[2]: 500k-arc KKT, two-pass
+    k = 500, f = inv) solved independently on every rank's GPU — one solve's units per GPU,
+    no collective (weak scaling) — K timed solves between barriers, max over ranks. Every
+    rank's x must carry the headline's committed digest (the same bits on every GPU: the
+    order is pinned). Returns the summary rank 0 prints (its own live roofline, and every
+    rank's pass-one step and k_p1_spmv beside it)."""
+    import numpy as np
+    import torch
+
+    import tpl_amd
+    from tpl_amd import _lib
+    from tpl_amd.error import check
+    stage_marker("replicas: operator")
+    kkt, data = load_workload(500000)
+    a = kkt.a
+    n = a.shape[0]
+    b = a @ np.full(n, 1.0 / np.sqrt(n))
+    op = tpl_amd.HipCsrOp(a, device=device)
+    if op.flags() & 64:
+        op.set_order_groups(PINNED_ORDER_GROUPS[500000])
+    bd = torch.from_numpy(np.ascontiguousarray(b)).cuda(device)
+    xd = torch.empty_like(bd)
+
+    def solve():
+        check(_lib.tpl_lanczos_two_pass(op.handle, bd.data_ptr(), n, args.k, _lib.FTK_INV_PTR,
+                                        None, xd.data_ptr(), _lib.TPL_MEM_DEVICE))
+    op.enable_timing(True)
+    for _ in range(max(args.warmup, 1)):
+        solve()
+    torch.cuda.synchronize()
+    dist.barrier()
+    stage_marker("replicas: timed_loop")
+    t0 = time.perf_counter()
+    per = []
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        solve()
+        per.append(time.perf_counter() - ts)
+    torch.cuda.synchronize()
+    dist.barrier()
+    dt = time.perf_counter() - t0
+    stage_marker("replicas: timed_done")
+    t = torch.tensor([dt], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dt = float(t.item())
+    p1_us, p2_us, p2_n = op.pass_timing()
+    try:
+        s1_us, a1_us, n_samp = op.step_samples()
+    except Exception:  # noqa: BLE001
+        s1_us = a1_us = None
+        n_samp = 0
+    steps = tpl_amd.algorithms.lanczos_pass_one(op, b, args.k).steps_taken
+    mine = {"rank": rank, "device": device, "x": x_digest(xd.cpu().numpy()),
+            "ms_per_solve_median": round(1000.0 * sorted(per)[len(per) // 2], 4),
+            "pass1_us_per_step": round(p1_us / steps, 3),
+            "k_p1_spmv_us": None if s1_us is None else round(s1_us, 3),
+            "k_p2_spmv_us": round(p2_us / p2_n, 3)}
+    every = [None] * world
+    dist.all_gather_object(every, mine)
+    b_spmv = op.algo_bytes(_lib.TPL_KERNEL_SPMV)
+    b_fused = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
+    pmc = {}
+    for name in ("pmc_k_p2_spmv.json", "pmc_pass_one.json"):
+        try:
+            with open(os.path.join(ROOT, "profiles", name)) as f:
+                pmc[name] = json.load(f)
+        except (OSError, ValueError):
+            pass
+    p2_tr = pmc.get("pmc_k_p2_spmv.json", {})
+    p1_tr = pmc.get("pmc_pass_one.json", {})
+    p1_traffic = {k.split("::")[-1].split("<")[0]: v["traffic_bytes_per_launch"]
+                  for k, v in p1_tr.get("kernels", {}).items()} or None
+    roof = roofline_block(b_spmv, b_fused, p2_us / p2_n, s1_us, a1_us, n_samp, steps,
+                          p1_us / steps, dt / args.steps, p2_tr.get("traffic_bytes_per_launch"),
+                          p2_tr.get("source"), p1_traffic, p1_tr.get("source"), {}, False)
+    roof["rank"] = 0
+    expected = expected_parity().get("headline", {}).get("x")
+    op.close()
+    del bd, xd
+    torch.cuda.empty_cache()
+    iters = world * args.steps * steps
+    return {"value": round(iters / dt, 2), "ms_per_step": round(1000.0 * dt / args.steps, 4),
+            "ms_per_solve_median": mine["ms_per_solve_median"] if rank == 0 else None,
+            "steps_taken": steps, "data": data, "n": n, "nnz": int(a.nnz), "roofline": roof,
+            "ranks": every,
+            "parity": {"ok": expected is not None and all(e["x"] == expected for e in every),
+                       "x_expected": expected, "x_every_rank": [e["x"] for e in every]}}
+
+
+def merge_replicas(rep: dict, part: dict, world: int, args) -> dict:
+    """The N > 1 line: `value` from the replicas (weak scaling of the headline), the
+    row-partitioned configs[4] solve of the same run under `partitioned_configs4`."""
+    line = {
+        "metric": METRIC, "value": rep["value"], "unit": "Lanczos iterations/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": rep["ms_per_step"],
+        "ms_per_solve_median": rep["ms_per_solve_median"], "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+        "data": rep["data"] + f"; the same solve on each of the {world} GPUs",
+        "config": {"workload": f"lanczos_two_pass k={args.k} f=inv, 500000-arc rho=3 KKT "
+                               f"(n={rep['n']}, nnz={rep['nnz']}), one independent solve per "
+                               f"GPU ({world} replicas, no collective)",
+                   "k": args.k, "steps_taken": rep["steps_taken"],
+                   "order_groups": PINNED_ORDER_GROUPS[500000],
+                   "parallelism": f"replicas{world} (weak scaling: the headline on every GPU)"},
+        "roofline": rep["roofline"], "ranks": rep["ranks"]}
+    parity = {"headline_replicas": rep["parity"]}
+    parity.update(part.get("parity", {}).get("workloads", {}))
+    line["parity"] = {"all_ok": all(v.get("ok") is True for v in parity.values()),
+                      "checked": len(parity), "workloads": parity,
+                      "source": part.get("parity", {}).get("source")}
+    keep = ("value", "unit", "ms_per_step", "ms_per_solve_median", "ms_per_solve_min",
+            "iterations_per_s_median", "config", "roofline", "exchange", "predicted",
+            "single_gpu_same_workload", "data")
+    line["partitioned_configs4"] = dict({k: part[k] for k in keep if k in part},
+                                        scaling="strong")
+    return line
+
+
 # ---- N > 1: the parent process (never touches the GPU) ------------------------------
 def stage_marker(stage: str) -> None:
     """Append this rank's progress to its marker file (TPL_BENCH_STAGE_DIR, set by the
@@ -487,6 +611,7 @@ def main():
 
     device = int(os.environ.get("TPL_DEVICE", local_rank))  # rehearsal: ranks sharing one GPU
     torch.cuda.set_device(device)
+    rep = run_replicas(args, rank, world, dist, device) if world > 1 and args.replicas else None
     partitioned = (world > 1) if args.partition < 0 else bool(args.partition)
     arcs = args.arcs or (ARCS_SCALE if partitioned else 500000)
     kkt, data = load_workload(arcs)
@@ -676,7 +801,9 @@ def main():
         "ms_per_solve_min": round(per_ms[0], 4),
         "iterations_per_s_median": round(steps_taken / (med_ms * 1e-3), 2),
         "higher_is_better": True,
-        "scaling": "strong",
+        # N = 1: one headline solve per GPU (the replicas' per-GPU work at N > 1); a
+        # partitioned solve: fixed total work over the ranks
+        "scaling": "strong" if partitioned else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": data,
@@ -917,6 +1044,8 @@ def main():
                       "tests/test_parity_digests.py)",
             "workloads": parity}
     if rank == 0:
+        if rep is not None:
+            out = merge_replicas(rep, out, world, args)
         stage_marker("report")
         print(json.dumps(out), flush=True)
     op.close()

@@ -175,3 +175,29 @@ def test_prediction_and_roofline_blocks(tmp_path, monkeypatch):
     r2 = bench.roofline_block(34e6, 40e6, 6.3, None, None, 0, 500, 11.1, 8.8e-3, None, None,
                               None, None, {}, True)
     assert r2["kernel"].startswith("k_p2_spmv") and "all_spmv_time_weighted_frac" not in r2
+
+
+def test_merge_replicas_line():
+    """N > 1: `value` is the replicas' weak-scaled headline throughput; the partitioned
+    configs[4] solve rides along under `partitioned_configs4` (strong scaling), and the
+    parity block covers both."""
+    import argparse
+    rep = {"value": 4 * 57000.0, "ms_per_step": 8.8, "ms_per_solve_median": 8.79,
+           "steps_taken": 500, "data": "netgen 500000-arc", "n": 501155, "nnz": 2000000,
+           "roofline": {"kernel": "k_p1_spmv", "frac": 0.65}, "ranks": [{}] * 4,
+           "parity": {"ok": True, "x_expected": "7bf2409fbbfac620",
+                      "x_every_rank": ["7bf2409fbbfac620"] * 4}}
+    part = {"value": 17000.0, "unit": "Lanczos iterations/s", "ms_per_step": 29.4,
+            "config": {"workload": "5M partitioned"}, "roofline": {"kernel": "k_p2_spmv"},
+            "predicted": {"implied_L_us": 10.0}, "exchange": {"comm_frac": 0.5},
+            "parity": {"source": "x", "workloads": {"configs4_replicated_N4": {"ok": True}}}}
+    args = argparse.Namespace(steps=5, warmup=1, k=500)
+    line = bench.merge_replicas(rep, part, 4, args)
+    assert line["value"] == 228000.0 and line["scaling"] == "weak" and line["n_gpus"] == 4
+    assert line["metric"] == bench.METRIC
+    assert line["partitioned_configs4"]["value"] == 17000.0
+    assert line["partitioned_configs4"]["scaling"] == "strong"
+    assert line["partitioned_configs4"]["predicted"]["implied_L_us"] == 10.0
+    assert line["parity"]["all_ok"] and line["parity"]["checked"] == 2
+    part["parity"]["workloads"]["configs4_replicated_N4"]["ok"] = False
+    assert not bench.merge_replicas(rep, part, 4, args)["parity"]["all_ok"]
