@@ -890,6 +890,7 @@ void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV,
   if (reorth) {
     enqueue_pass1(op, k, true, reorth); // eager: reorth launch counts vary with j
   } else {
+    op->p1_samples = 0;  // this pass records no launch stamps (tpl_op_step_samples)
     if (op->timing) HIPCHK(hipEventRecord(op->tev[0], op->stream));
     const int kind = storeV ? (elim ? kGStandardElim : kGStandard) : (elim ? kGPass1Elim : kGPass1);
     run_graph(op, kind, k, [&] { enqueue_pass1(op, k, storeV, false, elim); });
