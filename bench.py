@@ -854,6 +854,17 @@ def main():
         pred = predicted_block(world, args.k, steps_taken, solve_s)
         if pred is not None:
             out["predicted"] = pred
+    if not partitioned and world == 1 and not args.headline_only:
+        # the instrumentation's cost: the timed solves ran with live timing on (pass one
+        # stamped, the passes in three graphs with events between them); the same solve
+        # untimed is ONE graph
+        op.enable_timing(False)
+        tu = time_solves(solve, max(args.steps, 5), torch.cuda.synchronize)
+        op.enable_timing(True)
+        out["untimed_one_graph"] = {"ms_per_solve": round(1000.0 * tu, 4),
+                                    "iterations_per_s": round(steps_taken / tu, 2),
+                                    "note": "the same solve with live timing off (one device "
+                                            "graph, no events or stamps); not `value`"}
     if args.pcie and not partitioned and world == 1:
         # PCIe-inclusive rate (never `value`): host b in, host x out, one H2D + one D2H
         xh = np.empty(n)

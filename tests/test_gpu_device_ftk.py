@@ -140,6 +140,34 @@ def test_device_inv_timed_three_graphs(kkt5k):
     assert n2 == 49 and p1_us > 0 and p2_us > 0
 
 
+@pytest.mark.parametrize("k", [11, 50])
+def test_step_samples_live_pass_one(kkt50k, k):
+    """tpl_op_step_samples (round 5): the launch stamps of 8 middle steps of a timed
+    solve's pass-one graph give each kernel's start-to-start time; the two add up to the
+    pass-one step the events around the whole pass measure, and the stamped graph gives
+    the same bits as the untimed one-graph solve. A pass without stamps clears them."""
+    a = kkt50k.a
+    op = HipCsrOp(a)
+    b = harness_b(a)
+    x0 = solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    op.enable_timing(True)
+    with pytest.raises(tpl_amd.TplError):
+        op.step_samples()  # nothing timed yet
+    for _ in range(3):
+        x1 = solvers.lanczos_two_pass(op, b, k, ftk.INV)
+        assert same_bits(x0, x1)
+    s1, a1, ns = op.step_samples()
+    p1_us, _, _ = op.pass_timing()
+    assert ns == 8 and 0.5 < s1 < 100 and 0.5 < a1 < 100
+    # the stamped steps are middle steps; the pass mean includes the prologue and step 1
+    assert abs((s1 + a1) - p1_us / k) < 0.25 * (p1_us / k), (s1, a1, p1_us / k)
+    op.set_device_ftk(0)  # host f: pass one without stamps
+    solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    with pytest.raises(tpl_amd.TplError):
+        op.step_samples()
+    op.enable_timing(False)
+
+
 def test_device_inv_zero_b_error(kkt5k):
     op = HipCsrOp(kkt5k.a)
     with pytest.raises(LanczosError) as e:
