@@ -320,15 +320,17 @@ def predicted_block(world: int, k: int, steps: int, solve_s: float):
     if rs.get("k") != k or one.get("steps") != steps:
         return {"error": f"profile is for k={rs.get('k')}, steps={one.get('steps')}"}
     c = 2 * steps + (steps - 1)
-    t0 = one["ms_per_solve"]
+    # the N-rank solve runs at the pace of its slowest rank's share
+    t0 = max(sh.get("ms_per_solve_every_rank") or [one["ms_per_solve"]])
     return {"source": f"profiles/rank_share.json ({rs.get('source', 'scripts/rank_share.py')})",
             "rank0_rows": sh["rank0_rows"], "rank0_nnz": sh["rank0_nnz"],
+            "ms_every_rank_share": sh.get("ms_per_solve_every_rank"),
             "per_step_us_1rank": {"pass1": one["pass1_us_per_step"],
                                   "pass2": one["pass2_us_per_step"]},
             "exchange_1rank_us": one.get("exchange_1rank_us"),
             "single_gpu_same_share_ms": sh.get("single_gpu", {}).get("ms_per_solve"),
             "collectives_per_step": sh["collectives_per_step"], "collectives_per_solve": c,
-            "model": "ms = ms_1rank + collectives_per_solve * L / 1000",
+            "model": "ms = slowest rank's share (ms_1rank) + collectives_per_solve * L / 1000",
             "ms_1rank": t0,
             "ms_at_L_us": {str(L): round(t0 + c * L / 1000.0, 3) for L in (5, 10, 20, 40)},
             "measured_ms": round(1000.0 * solve_s, 3),
@@ -352,7 +354,7 @@ def predicted_curve(k: int, single_ms: float):
         sh = rs.get("shares", {}).get(n)
         if not sh:
             continue
-        t0 = sh["one_rank_replicated"]["ms_per_solve"]
+        t0 = max(sh.get("ms_per_solve_every_rank") or [sh["one_rank_replicated"]["ms_per_solve"]])
         c = sh["collectives_per_solve"]
         out["N"][n] = {"ms_1rank_share": t0, "kernels_only_speedup": round(single_ms / t0, 2),
                        **{f"L{L}us": {"ms": round(t0 + c * L / 1000.0, 2),
