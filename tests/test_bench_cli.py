@@ -166,6 +166,12 @@ def test_prediction_and_roofline_blocks(tmp_path, monkeypatch):
     assert "error" in bench.predicted_block(8, 400, 400, 0.03)
     c = bench.predicted_curve(500, 66.0)
     assert c["N"]["8"]["L10us"]["speedup"] == round(66.0 / (15.0 + 14.99), 2)
+    # every rank's share measured: the solve waits for the slowest
+    rs["shares"]["8"]["ms_per_solve_every_rank"] = [15.0, 16.5, 14.0]
+    f.write_text(json.dumps(rs))
+    p = bench.predicted_block(8, 500, 500, 0.030)
+    assert p["ms_1rank"] == 16.5 and p["ms_at_L_us"]["10"] == round(16.5 + 14.99, 3)
+    assert bench.predicted_curve(500, 66.0)["N"]["8"]["ms_1rank_share"] == 16.5
     r = bench.roofline_block(34e6, 40e6, 6.3, 6.5, 4.6, 8, 500, 11.1, 8.8e-3, 22e6, "p2",
                              {"k_p1_spmv": 19e6, "k_p1_axpy": 12e6}, "p1", {}, False)
     assert r["kernel"] == "k_p1_spmv" and r["avg_launch_us_events"] == 6.5
