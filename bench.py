@@ -109,6 +109,10 @@ def parse(argv=None):
                         "(weak scaling, no collective); the row-partitioned configs[4] solve "
                         "follows in the same run as `partitioned_configs4`. 0: `value` is the "
                         "partitioned solve itself")
+    p.add_argument("--rank-timeout", type=float, default=600.0,
+                   help="N > 1: seconds after which every rank gives up (a hung collective); "
+                        "rank 0 then prints the replicas' line with the partitioned phase "
+                        "marked timeout")
     p.add_argument("--dist-mode", choices=("auto", "replicated", "rows"), default="auto",
                    help="partition of the N > 1 solve: replicated long rows (auto: when the "
                         "matrix allows it) or row blocks with the whole vector all-gathered")
@@ -482,10 +486,52 @@ def merge_replicas(rep: dict, part: dict, world: int, args) -> dict:
     return line
 
 
+def partitioned_failure_line(rep: dict, world: int, args, status: str, detail: str) -> dict:
+    """The N > 1 line when the partitioned configs[4] phase failed or hung after the
+    replicas were measured: the replicas' `value` stands, the phase's status beside it."""
+    line = merge_replicas(rep, {}, world, args)
+    line["partitioned_configs4"] = {"status": status, "detail": detail,
+                                    "last_stage_rank0": _PROGRESS["stage"],
+                                    "after_s": round(time.time() - _PROGRESS["t0"], 1)}
+    line["parity"]["all_ok"] = False  # the partitioned digest was never checked
+    return line
+
+
+def rank_watchdog(rank: int, world: int, args):
+    """N > 1 under the driver's torchrun (no bench parent to time the ranks out): if the
+    run has not finished `args.rank_timeout` s after start — a hung collective — rank 0
+    prints the line it has (the replicas' value, the partitioned phase marked "timeout"
+    with the stage it reached) and every rank exits, instead of the job dying silently."""
+    import threading
+
+    def fire():
+        rep = _PROGRESS["replicas"]
+        if rank == 0:
+            if rep is not None:
+                line = partitioned_failure_line(rep, world, args, "timeout",
+                                                f"not finished after {args.rank_timeout} s")
+            else:
+                line = {"metric": METRIC, "value": None, "unit": "Lanczos iterations/s",
+                        "n_gpus": world, "higher_is_better": True, "status": "timeout",
+                        "last_stage_rank0": _PROGRESS["stage"],
+                        "after_s": round(time.time() - _PROGRESS["t0"], 1)}
+            print(json.dumps(line), flush=True)
+        os._exit(0 if rep is not None else 124)
+    t = threading.Timer(args.rank_timeout, fire)
+    t.daemon = True
+    t.start()
+    return t
+
+
 # ---- N > 1: the parent process (never touches the GPU) ------------------------------
+# this rank's progress, for the N > 1 watchdog (rank_watchdog)
+_PROGRESS = {"stage": "start", "t0": time.time(), "replicas": None}
+
+
 def stage_marker(stage: str) -> None:
     """Append this rank's progress to its marker file (TPL_BENCH_STAGE_DIR, set by the
     parent), so a hung or failed N-rank run still reports where every rank stopped."""
+    _PROGRESS["stage"] = stage
     d = os.environ.get("TPL_BENCH_STAGE_DIR")
     if not d:
         return
@@ -614,6 +660,7 @@ def main():
     device = int(os.environ.get("TPL_DEVICE", local_rank))  # rehearsal: ranks sharing one GPU
     torch.cuda.set_device(device)
     rep = run_replicas(args, rank, world, dist, device) if world > 1 and args.replicas else None
+    _PROGRESS["replicas"] = rep
     partitioned = (world > 1) if args.partition < 0 else bool(args.partition)
     arcs = args.arcs or (ARCS_SCALE if partitioned else 500000)
     kkt, data = load_workload(arcs)
@@ -1069,5 +1116,29 @@ def main():
         dist.destroy_process_group()
 
 
+def run():
+    """main() with the N > 1 safety net: a rank-local watchdog against hangs, and — when the
+    partitioned phase raises after the replicas were measured — rank 0's line with the
+    replicas' value and the error, instead of no line at all."""
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world <= 1 or "WORLD_SIZE" not in os.environ:
+        return main()
+    dog = rank_watchdog(rank, world, args)
+    try:
+        main()
+    except Exception as e:  # noqa: BLE001
+        rep = _PROGRESS["replicas"]
+        if rep is None:
+            raise
+        if rank == 0:
+            print(json.dumps(partitioned_failure_line(rep, world, args, "failed",
+                                                      f"{type(e).__name__}: {e}")), flush=True)
+        os._exit(0)  # peers blocked in a collective are ended by their own watchdogs
+    finally:
+        dog.cancel()
+
+
 if __name__ == "__main__":
-    main()
+    run()

@@ -2,6 +2,7 @@
 (the parent starts torch.distributed.run as a child — never an exec, never a GPU call —
 and exits with its status)."""
 import json
+import time
 import os
 import sys
 
@@ -207,3 +208,31 @@ def test_merge_replicas_line():
     assert line["parity"]["all_ok"] and line["parity"]["checked"] == 2
     part["parity"]["workloads"]["configs4_replicated_N4"]["ok"] = False
     assert not bench.merge_replicas(rep, part, 4, args)["parity"]["all_ok"]
+
+
+def test_rank_watchdog_prints_the_replicas_line(tmp_path):
+    """N > 1 under the driver's torchrun: a rank whose run has not finished by
+    --rank-timeout ends itself; rank 0 first prints the replicas' line with the
+    partitioned phase marked timeout (a hung collective leaves a line, not silence)."""
+    import subprocess
+    code = r"""
+import json, os, sys, time
+sys.path.insert(0, os.environ["BENCH_ROOT"])
+import bench, argparse
+args = argparse.Namespace(steps=5, warmup=1, k=500, rank_timeout=1.0)
+bench._PROGRESS["replicas"] = {"value": 2 * 57000.0, "ms_per_step": 8.8, "ms_per_solve_median": 8.8,
+    "steps_taken": 500, "data": "d", "n": 1, "nnz": 1, "roofline": {}, "ranks": [],
+    "parity": {"ok": True}}
+bench.stage_marker("partitioned: first_solve")
+bench.rank_watchdog(0, 2, args)
+time.sleep(30)  # a hung collective
+"""
+    t = time.time()
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
+                       env=dict(os.environ, BENCH_ROOT=ROOT))
+    assert p.returncode == 0 and time.time() - t < 20
+    line = json.loads(p.stdout.strip().splitlines()[-1])
+    assert line["value"] == 114000.0 and line["scaling"] == "weak"
+    pc = line["partitioned_configs4"]
+    assert pc["status"] == "timeout" and pc["last_stage_rank0"] == "partitioned: first_solve"
+    assert line["parity"]["all_ok"] is False
