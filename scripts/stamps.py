@@ -81,7 +81,8 @@ if os.environ.get("PASS1", "1") == "1":
             print(f"  {nm:5s} mark{k}-start {q(tt[:,k]-tt[:,0])}")
         print(f"  {nm:5s} end        {q(tt[:,5])} | dur {q(tt[:,5]-tt[:,0])}")
     print(f"  axpy  start      {q(ta[:,0])}   (gap after the SpMV's last end: {np.nanmin(ta[:,0]) - np.nanmax(ts[:,5]):.2f})")
-    for k, nm in [(1, "vectors in"), (2, "alpha known"), (3, "r stored")]:
+    for k, nm in [(1, "loads issued"), (4, "alpha partials landed"), (2, "alpha known"),
+                  (3, "r stored")]:
         print(f"  axpy  mark{k}-start {q(ta[:,k]-ta[:,0])}  ({nm})")
     print(f"  axpy  end        {q(ta[:,5])} | dur {q(ta[:,5]-ta[:,0])}")
 

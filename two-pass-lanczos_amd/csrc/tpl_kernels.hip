@@ -325,6 +325,12 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
   const int stop = S.flags[0];
   const double normj = S.norms[j - 1];
   TPL_MARK_AT(kAxpyMarkBase, 1);
+#if TPL_STAMP
+  // diagnostic build: when the alpha partials (issued first) have landed, the vector loads
+  // (2 kAxPairs issued after them) still in flight
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  TPL_MARK_AT(kAxpyMarkBase, 4);
+#endif
   // alpha while the vectors are in flight: its wait covers the partials (issued first)
   // only. The reduction's LDS stores and barrier keep the vector loads ahead of it, and
   // nothing tests the (uniform) stop flag before it: a branch there would let the compiler
