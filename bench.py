@@ -113,9 +113,11 @@ def parse(argv=None):
                    help="N > 1: seconds after which every rank gives up (a hung collective); "
                         "rank 0 then prints the replicas' line with the partitioned phase "
                         "marked timeout")
-    p.add_argument("--dist-mode", choices=("auto", "replicated", "rows"), default="auto",
+    p.add_argument("--dist-mode", choices=("auto", "replicated", "rows", "halo"),
+                   default="auto",
                    help="partition of the N > 1 solve: replicated long rows (auto: when the "
-                        "matrix allows it) or row blocks with the whole vector all-gathered")
+                        "matrix allows it), row blocks with the whole vector all-gathered, "
+                        "or row blocks exchanging only their halo (same bits as rows)")
     p.add_argument("--child-timeout", type=float, default=CHILD_TIMEOUT_S,
                    help="N>1: seconds the parent waits for the torchrun child")
     return p.parse_args(argv)
@@ -809,8 +811,9 @@ def main():
             for rows, xs in parts:
                 x_full[rows] = xs
             if args.parity and (arcs, args.k, args.f) == (ARCS_SCALE, 500, "inv"):
-                parity[f"configs4_{op.mode}_N{world}"] = parity_entry(
-                    expected, f"configs4_{op.mode}_N{world}", x=x_digest(x_full))
+                # halo row blocks reduce in the plain row blocks' order: the same digest
+                key = f"configs4_{'rows' if op.mode == 'halo' else op.mode}_N{world}"
+                parity[key] = parity_entry(expected, key, x=x_digest(x_full))
     if partitioned and args.single_ref:
         # the same workload on rank 0's GPU alone, for the speed-up of the partition, and
         # the partitioned x checked against it
@@ -871,8 +874,9 @@ def main():
                    # of one configuration (P0, include/tpl.h tpl_op_set_order_groups)
                    "x_sha256_16": x_digest(x_host),
                    "parallelism": "single" if not partitioned
-                   else (f"{op.mode}{world} (" + ("long-row partials all-gathered per SpMV"
-                         if op.mode == "replicated" else "vector all-gathered per SpMV")
+                   else (f"{op.mode}{world} (" + {"replicated": "long-row partials all-gathered per SpMV",
+                                                  "halo": "halo rows all-gathered per SpMV"}.get(
+                         op.mode, "vector all-gathered per SpMV")
                          + f", {dctx.transport})")},
         "roofline": roofline_block(b_spmv, b_fused, us, s1_us, a1_us, n_samp, steps_taken,
                                    p1_step_us, solve_s, traffic, traffic_src, p1_traffic,

@@ -384,6 +384,20 @@ tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t*
 tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t* row_ptr,
                                          const int32_t* col_idx, const double* vals,
                                          tpl_op_t* out);
+/* Halo-exchange row blocks (the general form of SURVEY.md §8(e) for matrices without
+ * the KKT structure), from the WHOLE matrix (every rank passes the same CSR): rank r
+ * holds the rows [starts[r], starts[r+1]) (starts NULL: the tpl_dist_partition split),
+ * exactly as tpl_dist_op_create_csr, but an SpMV moves only the halo — the rows of each
+ * block that another rank's rows reference (B_q for rank q, H = max_q |B_q|): each
+ * rank packs its B_r into its slot and the slots are all-gathered (8 H bytes per rank
+ * instead of 8 n / nranks; a banded matrix of half-bandwidth w has H <= 2w). Same
+ * rows, layout and reduction order as tpl_dist_op_create_csr over the same split, so
+ * alpha, beta, steps and x are bitwise those of the plain row blocks.
+ * Like the two partitions above, it spreads the reference's one sequential
+ * operator.apply (src/algorithms/mod.rs:177) over the ranks.                          */
+tpl_status tpl_dist_op_create_halo(tpl_dist_t d, int64_t n, const int64_t* starts,
+                                   const int64_t* row_ptr, const int32_t* col_idx,
+                                   const double* vals, tpl_op_t* out);
 /* Global row index of each entry of this operator's vectors (tpl_op_nrows entries). */
 tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows);
 
@@ -391,14 +405,16 @@ tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows);
  * The host half of tpl_op_create_csr (mode TPL_PLAN_SINGLE: auto locality order, its
  * group count pinned by order_groups > 0 as tpl_op_set_order_groups does; nranks 1,
  * rank 0), of tpl_dist_op_create_replicated (TPL_PLAN_REPLICATED) or of a row-block
- * rank with the tpl_dist_partition split (TPL_PLAN_ROWS), run by the same code: rank
+ * rank with the tpl_dist_partition split (TPL_PLAN_ROWS; TPL_PLAN_HALO: of
+ * tpl_dist_op_create_halo, whose tpl_kernel_algo_bytes of the exchange ids then give
+ * the halo's bytes without a GPU), run by the same code: rank
  * `rank` of `nranks`, its rows, order and SpMV layout, and nothing on a device. Only
  * the host introspection calls accept the returned handle — tpl_op_nrows, tpl_op_nnz,
  * tpl_op_flags, tpl_op_schedule, tpl_op_slices, tpl_op_permutation, tpl_op_local_rows,
  * tpl_op_order_groups, tpl_kernel_algo_bytes — every other call returns
  * TPL_ERR_INVALID_ARGUMENT; free it with tpl_op_destroy. The parity fixtures use it to
  * restate a run's reduction order on a host without a GPU (tests/golden/make_parity.py). */
-enum { TPL_PLAN_SINGLE = 0, TPL_PLAN_REPLICATED = 1, TPL_PLAN_ROWS = 2 };
+enum { TPL_PLAN_SINGLE = 0, TPL_PLAN_REPLICATED = 1, TPL_PLAN_ROWS = 2, TPL_PLAN_HALO = 3 };
 tpl_status tpl_plan_create(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
                            const double* vals, int mode, int nranks, int rank,
                            int32_t order_groups, tpl_op_t* out);

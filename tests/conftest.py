@@ -81,6 +81,35 @@ def load_kkt(arcs: int, tmpdir: str):
     return _KKT_CACHE[arcs]
 
 
+def banded_hub(n=20000, w=3, hub_every=997, hub_half=150, hub_step=7, seed=5):
+    """A symmetric, diagonally dominant banded matrix (half-bandwidth w, uniform random
+    values) with a long "hub" row every hub_every rows whose entries reach
+    hub_half * hub_step columns to either side: a matrix without the KKT structure, whose
+    row blocks need only a narrow halo (tpl_dist_op_create_halo) — and long rows (bins)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(seed)
+    rows, cols = [], []
+    for k in range(1, w + 1):
+        i = np.arange(n - k)
+        rows.append(i)
+        cols.append(i + k)
+    off = np.arange(1, hub_half + 1) * hub_step
+    for h in range(hub_every // 2, n, hub_every):
+        j = h + off[h + off < n]
+        rows.append(np.full(len(j), h))
+        cols.append(j)
+        j = h - off[h - off >= 0]
+        rows.append(j)
+        cols.append(np.full(len(j), h))
+    r, c = np.concatenate(rows), np.concatenate(cols)
+    up = sp.coo_matrix((rng.uniform(-1.0, 1.0, len(r)), (r, c)), shape=(n, n)).tocsr()
+    up.sum_duplicates()
+    a = up + up.T
+    a = (a + sp.diags(np.asarray(abs(a).sum(axis=1)).ravel() + 1.0)).tocsr()
+    a.sort_indices()
+    return a
+
+
 def harness_b(a):
     """b = A (1/sqrt(n)) 1, as src/bin/tradeoff.rs:235-236 (row-sequential sums)."""
     n = a.shape[0]

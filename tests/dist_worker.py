@@ -21,8 +21,9 @@ def main():
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     import tpl_amd
     from tpl_amd.dist import DistContext, DistHipCsrOp
-    from conftest import harness_b, load_kkt
-    a = load_kkt(arcs, out).a
+    from conftest import banded_hub, harness_b, load_kkt
+    # TPL_TEST_MATRIX=banded: tests/conftest.py banded_hub (no KKT structure) instead
+    a = banded_hub() if os.environ.get("TPL_TEST_MATRIX") == "banded" else load_kkt(arcs, out).a
     b = harness_b(a)
     ctx = DistContext(rank, world, device=int(os.environ.get("TPL_DEVICE", "0")), transport=transport)
     op = DistHipCsrOp(a, ctx, mode=mode)

@@ -4,8 +4,10 @@
   result bit for bit (same layout, the rank total of alpha/beta partials is exact);
   replicated long rows: within 1e-10;
 * two and three ranks sharing this box's GPU, exchanging through the host transport
-  (RCCL refuses two ranks on one device), both partitions: identical coefficients on
-  every rank, deterministic, x within 1e-10 of the single-GPU solve, SpMV blocks.
+  (RCCL refuses two ranks on one device), every partition: identical coefficients on
+  every rank, deterministic, x within 1e-10 of the single-GPU solve, SpMV blocks;
+* halo-exchange row blocks on a banded matrix without the KKT structure: bitwise the
+  plain row blocks' result and the restated partitioned order, moving only the halo.
 The ranks run as child processes (tests/dist_worker.py)."""
 import os
 import socket
@@ -60,10 +62,11 @@ def _assemble(rs, key, n):
     return out
 
 
-def test_one_rank_rccl_rows_bitwise(kkt_tmp, tmp_path):
+@pytest.mark.parametrize("mode", ["rows", "halo"])
+def test_one_rank_rccl_rows_bitwise(kkt_tmp, tmp_path, mode):
     a, x, dec, xs = _single(kkt_tmp)  # same layout as the partition's
-    r = _run_ranks(str(tmp_path), 1, "rccl", mode="rows")[0]
-    assert str(r["mode"]) == "rows"
+    r = _run_ranks(str(tmp_path), 1, "rccl", mode=mode)[0]
+    assert str(r["mode"]) == mode
     _check_exchange_profile([r])
     assert np.array_equal(r["x1"], x)
     assert np.array_equal(r["al"], dec.alphas) and np.array_equal(r["be"], dec.betas)
@@ -85,6 +88,8 @@ def _check_exchange_profile(rs):
             nl = len(r["s_long"])
             nch = max(-(-(len(q["rows"]) - nl) // 512) for q in rs)
             assert b2 == 8 * R * (nl + 1) and b1 == 8 * R * (nl + nch + 1)
+        elif str(r["mode"]) == "halo":  # the halo slots (none with one rank)
+            assert b1 - b2 == 16 * R and b2 % (8 * R) == 0 and (b2 > 0) == (R > 1)
         else:
             assert b1 - b2 == 16 * R and b2 > 0
 
@@ -129,7 +134,7 @@ def _check_partition_order(a, rs, mode, k):
         assert (ps["G2"], ps["E"], ps["slices"]) == (int(rec["s_G2"]), int(rec["s_E"]),
                                                      int(rec["s_slices"]))
         plan.close()
-    po = PartitionOracle(a, rs, mode)
+    po = PartitionOracle(a, rs, "rows" if mode == "halo" else mode)  # halo: rows' order
     al, be, s, bn = po.pass_one(b, k)
     assert int(rs[0]["steps"]) == s and float(rs[0]["bn"]) == bn
     assert np.array_equal(rs[0]["al"], al) and np.array_equal(rs[0]["be"], be)
@@ -138,7 +143,7 @@ def _check_partition_order(a, rs, mode, k):
 
 
 @pytest.mark.parametrize("world,mode", [(2, "rows"), (3, "rows"), (2, "replicated"),
-                                        (3, "replicated")])
+                                        (3, "replicated"), (2, "halo"), (3, "halo")])
 def test_ranks_share_gpu_host_transport(kkt_tmp, tmp_path, world, mode):
     a, x, dec, xs = _single(kkt_tmp)
     rs = _run_ranks(str(tmp_path), world, "host", mode=mode)
@@ -165,3 +170,32 @@ def test_ranks_share_gpu_host_transport(kkt_tmp, tmp_path, world, mode):
     y = _assemble(rs, "y", n)
     yr = a @ np.cos(np.arange(a.shape[0]))
     np.testing.assert_allclose(y, yr, rtol=1e-13, atol=1e-12)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_banded_host_transport(tmp_path, world):
+    """tpl_dist_op_create_halo on a matrix without the KKT structure (tests/conftest.py
+    banded_hub: band + long hub rows, general values): the same bits as the plain row
+    blocks and as the restated partitioned order, every rank receiving only the halo
+    (8 H bytes per rank and SpMV, H = dist.halo_width), and "auto" picks it."""
+    from conftest import banded_hub
+    from tpl_amd.dist import halo_width
+    env = {"TPL_TEST_MATRIX": "banded"}
+    a = banded_hub()
+    rows = _run_ranks(str(tmp_path / "rows"), world, "host", mode="rows", extra_env=env)
+    halo = _run_ranks(str(tmp_path / "halo"), world, "host", mode="auto", extra_env=env)
+    assert all(str(r["mode"]) == "halo" for r in halo)
+    for rr, rh in zip(rows, halo):
+        for key in ("rows", "x1", "x2", "x3", "xs", "al", "be", "y"):
+            assert np.array_equal(rr[key], rh[key]), key
+    H = halo_width(a, halo[0]["starts"])
+    assert 0 < H < a.shape[0] // (2 * world)
+    for r in halo:
+        b1, b2 = r["ex_bytes"]
+        assert b2 == 8 * world * H and b1 == 8 * world * (H + 2)
+    for r in rows:
+        assert r["ex_bytes"][1] > 8 * world * a.shape[0] // world - 1
+    _check_partition_order(a, halo, "halo", 50)
+    y = _assemble(halo, "y", a.shape[0])
+    yr = a @ np.cos(np.arange(a.shape[0]))
+    np.testing.assert_allclose(y, yr, rtol=1e-12, atol=1e-12)

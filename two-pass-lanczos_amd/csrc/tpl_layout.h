@@ -55,10 +55,14 @@ struct Layout {
 // Column index as stored on the device: the identity on one GPU; with the rows
 // partitioned over ranks, global column c (owned by rank r, rows [starts[r],
 // starts[r+1])) lives at r * ld + (c - starts[r]) of the all-gathered vector.
+// Halo-exchange row blocks: an explicit table (global column -> position in
+// [own block | nranks x halo slots]).
 struct ColMap {
   const std::vector<int64_t>* starts = nullptr;  // row partition (nullptr: see table)
   int64_t ld = 0;
+  const std::vector<int32_t>* table = nullptr;   // halo partition
   int32_t operator()(int32_t c) const {
+    if (table) return (*table)[c];
     if (!starts) return c;
     const auto it = std::upper_bound(starts->begin(), starts->end(), (int64_t)c);
     const int64_t r = (it - starts->begin()) - 1;

@@ -189,6 +189,14 @@ struct tpl_op_s {
   int32_t y_ld1 = 0;                // n_long + the most chunks of any rank
   std::vector<int32_t> nch;         // chunks (alpha partials) of every rank
   int32_t* d_nch = nullptr;
+  // halo-exchange row blocks (tpl_dist_op_create_halo): the gathered vector is
+  // [own block (ld) | nranks x hH halo slots]; rank q's slot holds the hH_q <= hH rows of
+  // its block that some other rank's rows reference (halo_send: their local indices),
+  // packed before each all-gather; halo_map: global column -> device position
+  bool halo = false;
+  int64_t hH = 0;
+  std::vector<int32_t> halo_send, halo_map;
+  int32_t* d_halo_send = nullptr;
   std::vector<int32_t> h_rowptr;
   std::vector<int32_t> h_col;
   std::vector<double> h_val;
@@ -340,7 +348,9 @@ void upload(tpl_op_s* op, T** dst, const std::vector<T>& src) {
 
 void rebuild_schedule(tpl_op_s* op) {
   ColMap cmap;
-  if (op->dist && !op->hybrid) {
+  if (op->halo) {
+    cmap.table = &op->halo_map;
+  } else if (op->dist && !op->hybrid) {
     cmap.starts = &op->starts;
     cmap.ld = op->ld;
   }
@@ -572,6 +582,20 @@ void dist_allgather(tpl_op_s* op, double* base, size_t count) {
                         op->stream));
   HIPCHK(hipStreamSynchronize(op->stream));
 }
+// Row blocks: complete the gather source G of this rank's SpMV. Plain row blocks
+// all-gather every rank's whole block (ld doubles each, in place); halo blocks first pack
+// the rows other ranks reference into this rank's halo slot (halo_pack, k_permute — issued
+// before the collective group) and all-gather the slots only (hH doubles each).
+void halo_pack(tpl_op_s* op, double* G) {
+  if (!op->halo || op->halo_send.empty()) return;
+  HIPCHK(launch::permute((int64_t)op->halo_send.size(), 1,
+                         G + op->ld + (size_t)op->dist->rank * op->hH, 0, G, 0,
+                         op->d_halo_send, op->stream));
+}
+void gather_vec(tpl_op_s* op, double* G) {
+  if (!op->halo) dist_allgather(op, G, (size_t)op->ld);
+  else if (op->hH > 0) dist_allgather(op, G + op->ld, (size_t)op->hH);
+}
 void dist_group(tpl_op_s* op, bool begin) {
   if (op->dist && op->dist->comm) NCCLCHK(begin ? ncclGroupStart() : ncclGroupEnd());
 }
@@ -626,9 +650,10 @@ void enqueue_p1_prologue(tpl_op_s* op) {
   } else if (op->dist) {
     const int R = op->dist->nranks;
     dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
+    halo_pack(op, op->bG);
     dist_group(op, true);
     dist_allgather(op, op->d_rsum + R, 1);
-    dist_allgather(op, op->bG, (size_t)op->ld);
+    gather_vec(op, op->bG);
     dist_group(op, false);
   }
 }
@@ -658,9 +683,10 @@ void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
   } else {
     const int R = op->dist->nranks;
     dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
+    halo_pack(op, op->RG[(j + 1) % 3]);
     dist_group(op, true);
     dist_allgather(op, op->d_rsum + R, 1);
-    dist_allgather(op, op->RG[(j + 1) % 3], (size_t)op->ld);
+    gather_vec(op, op->RG[(j + 1) % 3]);
     dist_group(op, false);
   }
 }
@@ -670,7 +696,8 @@ void enqueue_p2_exchange(tpl_op_s* op, int j) {
     const size_t nl = op->lay.lrows.size();
     if (nl) dist_allgather(op, op->d_yall, nl + 1);
   } else {
-    dist_allgather(op, op->V2G[(j + 1) % 3], (size_t)op->ld);
+    halo_pack(op, op->V2G[(j + 1) % 3]);
+    gather_vec(op, op->V2G[(j + 1) % 3]);
   }
 }
 
@@ -715,7 +742,10 @@ void enqueue_pass1(tpl_op_s* op, size_t k, bool storeV, int reorth, bool elim = 
 void enqueue_pass2_init(tpl_op_s* op, size_t steps, double* Vout) {
   HIPCHK(launch::p2_init(op->n, op->S, op->b, op->V2[1], op->x, Vout, 0, op->stream));
   HIPCHK(launch::p2_coefs(op->S, (int)steps, 0, op->stream));
-  if (op->dist && !op->hybrid) dist_allgather(op, op->V2G[1], (size_t)op->ld);
+  if (op->dist && !op->hybrid) {
+    halo_pack(op, op->V2G[1]);
+    gather_vec(op, op->V2G[1]);
+  }
 }
 void enqueue_pass2_steps(tpl_op_s* op, size_t steps, double* Vout) {
   const CsrDev A = csr_dev(op);
@@ -933,6 +963,10 @@ void zero_out(tpl_op_s* op, double* x_out, int mem) {
 // of a partition; the vector stride ld is common to all ranks).
 // Vector stride ld, common to all ranks (the gathered vector holds rank r's block at r * ld).
 void set_stride(tpl_op_s* op) {
+  if (op->halo) {  // [own block | nranks x hH halo slots]; fill_halo sized and checked it
+    op->ld = ((std::max<int64_t>(op->n, 1) + 63) / 64) * 64;
+    return;
+  }
   const int R = op->dist && !op->hybrid ? op->dist->nranks : 1;  // gathered vector copies
   int64_t widest = op->n;
   if (op->dist && !op->hybrid)
@@ -947,13 +981,14 @@ void init_op(tpl_op_s* op) {
   const int R = op->dist && !op->hybrid ? op->dist->nranks : 1;  // gathered vector copies
   set_stride(op);
   rebuild_schedule(op);
-  // gathered: b, R0..2, V2_0..2, tmp (R x ld each); local: W, x (ld each)
-  const size_t gathered = 8 * (size_t)R * op->ld, local = 2 * (size_t)op->ld;
+  // gathered: b, R0..2, V2_0..2, tmp (R x ld each; halo: ld + R x hH); local: W, x (ld each)
+  const size_t gl = op->halo ? (size_t)op->ld + (size_t)R * op->hH : (size_t)R * op->ld;
+  const size_t gathered = 8 * gl, local = 2 * (size_t)op->ld;
   dev_alloc(op, &op->d_vecs, (gathered + local) * sizeof(double));
   HIPCHK(hipMemset(op->d_vecs, 0, (gathered + local) * sizeof(double)));
   double* p = op->d_vecs;
-  const size_t gl = (size_t)R * op->ld;
-  const size_t own = (size_t)(op->dist && !op->hybrid ? op->dist->rank : 0) * op->ld;
+  const size_t own = (size_t)(op->dist && !op->hybrid && !op->halo ? op->dist->rank : 0) * op->ld;
+  upload(op, &op->d_halo_send, op->halo_send);
   op->bG = p;
   p += gl;
   for (int i = 0; i < 3; ++i, p += gl) op->RG[i] = p;
@@ -1113,6 +1148,73 @@ void fill_replicated(tpl_op_s* op, int R, int me, int64_t n, const int64_t* row_
     op->nch[r] = (int32_t)((cut[r + 1] - cut[r] + kChunkRows - 1) / kChunkRows);
 }
 
+// Host half of a row-block rank from the WHOLE matrix (TPL_PLAN_ROWS, TPL_PLAN_HALO,
+// tpl_dist_op_create_halo): block `me` of `starts` (nullptr: the tpl_dist_partition
+// split), its rows with global column indices. halo: also the halo plan — B_q = the rows
+// of rank q's block that a row of another rank references (one pass over the nonzeros),
+// hH = max_q |B_q|, this rank's send list (B_me in local indices) and the column table:
+// own column c -> c - starts[me], remote column c in B_q -> ld + q hH + (c's rank in B_q).
+// The layout is built from the same CSR and global-column slices as plain row blocks, so
+// the two hold the same reduction order; only the gathered positions differ.
+void fill_rows(tpl_op_s* op, int R, int me, int64_t n, const int64_t* starts,
+               const int64_t* row_ptr, const int32_t* col_idx, const double* vals, bool halo) {
+  if (n < R) fail(TPL_ERR_INVALID_ARGUMENT, "fewer rows than ranks");
+  if (n >= INT32_MAX / 2) fail(TPL_ERR_UNSUPPORTED, "n must be < 2^30");
+  if (row_ptr[0] != 0) fail(TPL_ERR_INVALID_ARGUMENT, "row_ptr must start at 0");
+  if (row_ptr[n] > 0 && (!vals || !col_idx)) fail(TPL_ERR_INVALID_ARGUMENT, "col_idx/vals is NULL");
+  check_csr(n, n, row_ptr, col_idx);
+  op->starts.resize(R + 1);
+  if (starts) {
+    if (starts[0] != 0 || starts[R] != n) fail(TPL_ERR_INVALID_ARGUMENT, "bad partition");
+    for (int r = 0; r < R; ++r)
+      if (starts[r + 1] <= starts[r]) fail(TPL_ERR_INVALID_ARGUMENT, "empty or unordered block");
+    op->starts.assign(starts, starts + R + 1);
+  } else {
+    std::vector<double> prefix(n + 1);
+    for (int64_t i = 0; i <= n; ++i) prefix[i] = 12.0 * (double)row_ptr[i] + 40.0 * (double)i;
+    balanced_cuts(prefix, R, op->starts.data());
+  }
+  const int64_t r0 = op->starts[me], r1 = op->starts[me + 1];
+  op->n = r1 - r0;
+  op->n_glob = n;
+  op->nnz = row_ptr[r1] - row_ptr[r0];
+  if (op->nnz >= INT32_MAX) fail(TPL_ERR_UNSUPPORTED, "nnz must be < 2^31");
+  op->h_rowptr.resize(op->n + 1);
+  for (int64_t i = 0; i <= op->n; ++i) op->h_rowptr[i] = (int32_t)(row_ptr[r0 + i] - row_ptr[r0]);
+  op->h_col.assign(col_idx + row_ptr[r0], col_idx + row_ptr[r1]);
+  op->h_val.assign(vals + row_ptr[r0], vals + row_ptr[r1]);
+  if (!halo) return;
+  const std::vector<int64_t>& st = op->starts;
+  std::vector<uint8_t> need(n, 0);
+  for (int r = 0; r < R; ++r)
+    for (int64_t q = row_ptr[st[r]]; q < row_ptr[st[r + 1]]; ++q) {
+      const int32_t c = col_idx[q];
+      if (c < st[r] || c >= st[r + 1]) need[c] = 1;
+    }
+  std::vector<int32_t> pos(n, -1);
+  int64_t H = 0;
+  for (int q = 0; q < R; ++q) {
+    int32_t m = 0;
+    for (int64_t c = st[q]; c < st[q + 1]; ++c)
+      if (need[c]) pos[c] = m++;
+    H = std::max<int64_t>(H, m);
+  }
+  op->halo = true;
+  op->hH = H;
+  const int64_t ld = ((std::max<int64_t>(op->n, 1) + 63) / 64) * 64;  // set_stride's
+  if (ld + (int64_t)R * H >= (int64_t)INT32_MAX)
+    fail(TPL_ERR_UNSUPPORTED, "halo partition: own block + nranks x halo width >= 2^31");
+  op->halo_send.clear();
+  for (int64_t c = r0; c < r1; ++c)
+    if (need[c]) op->halo_send.push_back((int32_t)(c - r0));
+  op->halo_map.assign(n, -1);
+  for (int64_t c = r0; c < r1; ++c) op->halo_map[c] = (int32_t)(c - r0);
+  for (int q = 0; q < R; ++q)
+    if (q != me)
+      for (int64_t c = st[q]; c < st[q + 1]; ++c)
+        if (pos[c] >= 0) op->halo_map[c] = (int32_t)(ld + (int64_t)q * H + pos[c]);
+}
+
 } // namespace
 
 // =========================================================== C ABI
@@ -1253,7 +1355,10 @@ tpl_status tpl_op_apply(tpl_op_t op, const double* x, double* y, int mem) {
     set_device(op);
     if (op->n == 0) return;
     upload_vec(op, op->tmp, x, mem);
-    if (op->dist && !op->hybrid) dist_allgather(op, op->tmpG, (size_t)op->ld);
+    if (op->dist && !op->hybrid) {
+      halo_pack(op, op->tmpG);
+      gather_vec(op, op->tmpG);
+    }
     const CsrDev A = csr_dev(op);
     HIPCHK(launch::spmv(A, op->tmpG, op->W, op->stream));
     if (op->hybrid && A.n_long > 0) {
@@ -1613,9 +1718,9 @@ double tpl_kernel_algo_bytes(tpl_op_t op, int kernel) {
         return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (op->y_ld1 + 1.0)
                                                 : 8.0 * R * (nl + 1.0);
       }
-      const double vec = (double)op->ld;
-      // pass one: the alpha and beta totals and one vector part per rank; pass two: the
-      // vector part only (the row-block pass two gathers v, no totals)
+      const double vec = (double)(op->halo ? op->hH : op->ld);
+      // pass one: the alpha and beta totals and one vector part per rank (halo: its halo
+      // slot); pass two: the vector part only (the row-block pass two gathers v, no totals)
       return kernel == TPL_KERNEL_EXCHANGE_P1 ? 8.0 * R * (vec + 2.0) : 8.0 * R * vec;
     }
     default: return 0.0;
@@ -2009,6 +2114,24 @@ tpl_status tpl_dist_op_create_csr(tpl_dist_t d, int64_t n_global, const int64_t*
 }
 
 
+tpl_status tpl_dist_op_create_halo(tpl_dist_t d, int64_t n, const int64_t* starts,
+                                   const int64_t* row_ptr, const int32_t* col_idx,
+                                   const double* vals, tpl_op_t* out) {
+  return guarded([&] {
+    if (!d || !row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    HIPCHK(hipSetDevice(d->ctx.device));
+    auto op = std::make_unique<tpl_op_s>();
+    op->ctx = &d->ctx;
+    op->device = d->ctx.device;
+    op->stream = d->ctx.stream;
+    op->dist = d;
+    op->eager = d->comm == nullptr;
+    fill_rows(op.get(), d->nranks, d->rank, n, starts, row_ptr, col_idx, vals, true);
+    init_op(op.get());
+    *out = op.release();
+  });
+}
+
 tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t* row_ptr,
                                          const int32_t* col_idx, const double* vals,
                                          tpl_op_t* out) {
@@ -2045,8 +2168,9 @@ tpl_status tpl_plan_create(int64_t n, const int64_t* row_ptr, const int32_t* col
                            int32_t order_groups, tpl_op_t* out) {
   return guarded([&] {
     if (!row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
-    if (mode < TPL_PLAN_SINGLE || mode > TPL_PLAN_ROWS)
-      fail(TPL_ERR_INVALID_ARGUMENT, "plan mode must be TPL_PLAN_SINGLE, _REPLICATED or _ROWS");
+    if (mode < TPL_PLAN_SINGLE || mode > TPL_PLAN_HALO)
+      fail(TPL_ERR_INVALID_ARGUMENT,
+           "plan mode must be TPL_PLAN_SINGLE, _REPLICATED, _ROWS or _HALO");
     if (mode == TPL_PLAN_SINGLE ? (nranks != 1 || rank != 0)
                                 : (nranks < 1 || rank < 0 || rank >= nranks))
       fail(TPL_ERR_INVALID_ARGUMENT, "bad rank / nranks");
@@ -2073,23 +2197,10 @@ tpl_status tpl_plan_create(int64_t n, const int64_t* row_ptr, const int32_t* col
       op->dist = op->plan_dist.get();
       if (mode == TPL_PLAN_REPLICATED) {
         fill_replicated(op.get(), nranks, rank, n, row_ptr, col_idx, vals);
-      } else {  // the block tpl_dist_partition gives this rank (tpl_dist_op_create_csr)
-        if (n < nranks) fail(TPL_ERR_INVALID_ARGUMENT, "fewer rows than ranks");
-        if (n >= INT32_MAX / 2) fail(TPL_ERR_UNSUPPORTED, "n must be < 2^30");
-        check_csr(n, n, row_ptr, col_idx);
-        std::vector<double> prefix(n + 1);
-        for (int64_t i = 0; i <= n; ++i) prefix[i] = 12.0 * (double)row_ptr[i] + 40.0 * (double)i;
-        op->starts.resize(nranks + 1);
-        balanced_cuts(prefix, nranks, op->starts.data());
-        const int64_t r0 = op->starts[rank], r1 = op->starts[rank + 1];
-        op->n = r1 - r0;
-        op->n_glob = n;
-        op->nnz = row_ptr[r1] - row_ptr[r0];
-        if (op->nnz >= INT32_MAX) fail(TPL_ERR_UNSUPPORTED, "nnz must be < 2^31");
-        op->h_rowptr.resize(op->n + 1);
-        for (int64_t i = 0; i <= op->n; ++i) op->h_rowptr[i] = (int32_t)(row_ptr[r0 + i] - row_ptr[r0]);
-        op->h_col.assign(col_idx + row_ptr[r0], col_idx + row_ptr[r1]);
-        op->h_val.assign(vals + row_ptr[r0], vals + row_ptr[r1]);
+      } else {  // the block tpl_dist_partition gives this rank (tpl_dist_op_create_csr /
+                // tpl_dist_op_create_halo)
+        fill_rows(op.get(), nranks, rank, n, nullptr, row_ptr, col_idx, vals,
+                  mode == TPL_PLAN_HALO);
       }
     }
     set_stride(op.get());

@@ -203,11 +203,14 @@ tpl_dist_op_create_csr = _sig("tpl_dist_op_create_csr", c_int, c_void_p, c_int64
                               POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p))
 tpl_dist_op_create_replicated = _sig("tpl_dist_op_create_replicated", c_int, c_void_p, c_int64,
                                      POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p))
+tpl_dist_op_create_halo = _sig("tpl_dist_op_create_halo", c_int, c_void_p, c_int64, POINTER(c_int64),
+                               POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p))
 tpl_op_local_rows = _sig("tpl_op_local_rows", c_int, c_void_p, POINTER(c_int64))
 # host-only plans (include/tpl.h "host-only plans")
-TPL_PLAN_SINGLE, TPL_PLAN_REPLICATED, TPL_PLAN_ROWS = 0, 1, 2
+TPL_PLAN_SINGLE, TPL_PLAN_REPLICATED, TPL_PLAN_ROWS, TPL_PLAN_HALO = 0, 1, 2, 3
 tpl_plan_create = _sig("tpl_plan_create", c_int, c_int64, POINTER(c_int64), POINTER(c_int32), PD,
                        c_int, c_int, c_int, c_int32, POINTER(c_void_p))
 EXPORTED += ["tpl_plan_create"]
 EXPORTED += ["tpl_dist_op_create_replicated", "tpl_op_local_rows", "tpl_dist_partition", "tpl_dist_unique_id", "tpl_dist_create",
-             "tpl_dist_create_host", "tpl_dist_destroy", "tpl_dist_op_create_csr"]
+             "tpl_dist_create_host", "tpl_dist_destroy", "tpl_dist_op_create_csr",
+             "tpl_dist_op_create_halo"]

@@ -2,7 +2,8 @@
 
 One process per GPU. Rank r owns the rows [starts[r], starts[r+1]) of A (contiguous
 blocks balanced by algorithmic bytes, ``partition``); each SpMV all-gathers the
-vector in place over RCCL/xGMI and alpha/beta combine the ranks' totals in rank
+vector in place over RCCL/xGMI — the whole blocks ("rows") or only the rows another
+rank references ("halo") — and alpha/beta combine the ranks' totals in rank
 order, so every rank holds the same alpha, beta and steps bit for bit. The solver
 entry points (``tpl_amd.lanczos_two_pass``, ``algorithms.*``) take a ``DistHipCsrOp``
 unchanged; ``b`` and the returned ``x`` are then this rank's block of rows.
@@ -21,6 +22,21 @@ import numpy as np
 from . import _lib
 from .error import check
 from .operator import HipCsrOp, _as_csr_arrays
+
+
+def halo_width(a, starts) -> int:
+    """H = max over ranks q of |B_q|, B_q = the rows of q's block [starts[q], starts[q+1])
+    that a row of another block references: the doubles per rank a halo all-gather moves
+    (tpl_dist_op_create_halo computes the same on the host side of the ABI)."""
+    n, rp, ci, _ = _as_csr_arrays(a)
+    starts = np.asarray(starts, dtype=np.int64)
+    row_owner = np.repeat(np.searchsorted(starts, np.arange(n), "right") - 1, np.diff(rp))
+    col_owner = np.searchsorted(starts, ci, "right") - 1
+    need = np.unique(ci[row_owner != col_owner])
+    if need.size == 0:
+        return 0
+    return int(np.bincount(np.searchsorted(starts, need, "right") - 1,
+                           minlength=len(starts) - 1).max())
 
 
 def partition(a, nranks: int) -> np.ndarray:
@@ -91,8 +107,11 @@ class DistHipCsrOp(HipCsrOp):
     mode "replicated" (tpl_dist_op_create_replicated): short rows in byte-balanced
     blocks, long rows replicated on every rank, n_long partials exchanged per SpMV;
     mode "rows" (tpl_dist_op_create_csr): contiguous row blocks, the whole vector
-    all-gathered per SpMV; "auto": replicated when the matrix allows it (no short row
-    references another rank's short rows — the KKT case), else rows.
+    all-gathered per SpMV; mode "halo" (tpl_dist_op_create_halo): the same blocks and
+    bits, only the rows another rank references all-gathered (``halo_width`` per rank);
+    "auto": replicated when the matrix allows it (no short row references another
+    rank's short rows — the KKT case), else halo when its width is at most half the
+    widest block (a banded or mesh-like matrix), else rows.
     ``local_rows``: global row of each entry of this rank's vectors (``local(v)``).
     """
 
@@ -115,6 +134,17 @@ class DistHipCsrOp(HipCsrOp):
         if self.mode is None:
             self.starts = (partition((n, rp, ci, v), ctx.world) if starts is None
                            else np.ascontiguousarray(starts, dtype=np.int64))
+        if self.mode is None and mode in ("auto", "halo"):
+            if mode == "halo" or 2 * halo_width((n, rp, ci, v), self.starts) <= int(
+                    np.diff(self.starts).max()):
+                check(_lib.tpl_dist_op_create_halo(
+                    ctx.handle, n, self.starts.ctypes.data_as(POINTER(c_int64)),
+                    rp.ctypes.data_as(POINTER(c_int64)), ci.ctypes.data_as(POINTER(c_int32)),
+                    v.ctypes.data_as(POINTER(c_double)), byref(h)))
+                self.mode = "halo"
+        if self.mode is None:
+            if mode not in ("auto", "rows", "replicated"):
+                raise ValueError(f"unknown partition mode {mode!r}")
             r0, r1 = int(self.starts[ctx.rank]), int(self.starts[ctx.rank + 1])
             lrp = np.ascontiguousarray(rp[r0:r1 + 1] - rp[r0], dtype=np.int64)
             lci = np.ascontiguousarray(ci[rp[r0]:rp[r1]], dtype=np.int32)

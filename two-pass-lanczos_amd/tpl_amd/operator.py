@@ -77,11 +77,11 @@ def _is_torch_cuda(x) -> bool:
 class HostPlan:
     """The host half of an operator (tpl_plan_create): rows, order and SpMV layout of a
     single-GPU operator (``mode="single"``, ``order_groups`` as set_order_groups) or of
-    rank ``rank`` of a partition (``"replicated"`` / ``"rows"``), computed by the
+    rank ``rank`` of a partition (``"replicated"`` / ``"rows"`` / ``"halo"``), computed by the
     runtime's own code with no GPU. ``schedule()`` and ``local_rows`` are what the live
     operator would report; every device call on it fails."""
 
-    _MODES = {"single": 0, "replicated": 1, "rows": 2}
+    _MODES = {"single": 0, "replicated": 1, "rows": 2, "halo": 3}
 
     def __init__(self, a, mode: str = "single", nranks: int = 1, rank: int = 0,
                  order_groups: int = 0):
@@ -109,6 +109,10 @@ class HostPlan:
 
     def order_groups(self) -> int:
         return int(_lib.tpl_op_order_groups(self._op))
+
+    def algo_bytes(self, kernel: int) -> float:
+        """tpl_kernel_algo_bytes: e.g. the bytes a rank receives per exchange."""
+        return float(_lib.tpl_kernel_algo_bytes(self._op, int(kernel)))
 
     def close(self):
         if getattr(self, "_op", None):
