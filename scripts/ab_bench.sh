@@ -1,12 +1,13 @@
 #!/bin/bash
 # A/B of library variants on one box: the quick headline bench (no side legs) for the
-# in-tree library and each variants/libtpl_<name>.so given, alternated REPS times.
+# in-tree library and each $VDIR/libtpl_<name>.so given (default
+# two-pass-lanczos_amd/variants), alternated REPS times.
 set -u
 ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$ROOT"
 for rep in $(seq 1 ${REPS:-2}); do
   for v in base "$@"; do
-    if [ "$v" = base ]; then lib=""; else lib="TPL_LIB_PATH=$ROOT/two-pass-lanczos_amd/variants/libtpl_$v.so"; fi
+    if [ "$v" = base ]; then lib=""; else lib="TPL_LIB_PATH=$ROOT/${VDIR:-two-pass-lanczos_amd/variants}/libtpl_$v.so"; fi
     out=$(env $lib timeout -k 10 300 python bench.py --other-configs 0 --one-pass 0 --pcie 0 --scale-ref 0 --cpu-baseline 0 --steps 10 2>/dev/null | tail -1)
     python3 -c "import json,sys; d=json.loads(sys.argv[1]); r=d['roofline']; print('$v', d['ms_per_solve_median'], r['pass1_us_per_step'], r['avg_launch_us_events'], r['kernels_us_isolated'], d['config']['x_sha256_16'])" "$out"
   done

@@ -201,6 +201,34 @@ static void layout_checks() {
     CHECK(seen_short == want_short && seen_long == want_long, "entries n=%lld: short %lld/%lld long %lld/%lld",
           (long long)c.n, (long long)seen_short, (long long)want_short, (long long)seen_long,
           (long long)want_long);
+    // the bin tables: each long row's packed pieces are its pieces with entries (one
+    // empty piece for a row with none), every one carrying that count - 1 (its arrival
+    // count, BinSeg::pad)
+    {
+      std::vector<int32_t> got(L.lrows.size(), 0), pad(L.lrows.size(), -1);
+      bool pad_ok = true;
+      for (size_t bin = 0; bin < nbins && !L.lrows.empty(); ++bin)
+        for (int j = 0; j < tpl::kTPB; ++j) {
+          const tpl::BinSeg& g = L.b_seg[bin * tpl::kTPB + j];
+          if (g.ri < 0) continue;
+          ++got[g.ri];
+          pad_ok = pad_ok && (pad[g.ri] < 0 || pad[g.ri] == g.pad);
+          pad[g.ri] = g.pad;
+        }
+      for (size_t r = 0; r < L.lrows.size(); ++r) {
+        const int32_t row = L.lrows[r];
+        int want = 0;
+        for (int s = 0; s < L.nslices; ++s) {
+          const int64_t lo = (int64_t)c.n * s / L.nslices, hi = (int64_t)c.n * (s + 1) / L.nslices;
+          int cnt = 0;
+          for (int32_t q = rp[row]; q < rp[row + 1]; ++q) cnt += col[q] >= lo && col[q] < hi;
+          want += cnt > 0;
+        }
+        want = std::max(want, 1);
+        pad_ok = pad_ok && got[r] == want && pad[r] == want - 1;
+      }
+      CHECK(pad_ok, "bin pieces / arrival counts n=%lld", (long long)c.n);
+    }
     // the locality order (a permutation, long rows last) and P A P^T (same entries,
     // columns ascending), then the layout of P A P^T
     for (int groups : {1, 16, 1000}) {

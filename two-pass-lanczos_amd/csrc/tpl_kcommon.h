@@ -649,7 +649,10 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   if (sg.ri < 0) return; // no piece for this thread
   const double p = psum[t];
   const int ns = A.n_slices;
-  if (ns == 1) {  // the piece is the whole row: no hand-off
+  // sg.pad = the row's packed pieces - 1 (only pieces with entries are packed; the
+  // slots of the others are never written and hold +0.0). One piece: it is the whole row
+  // (0 + p, then + 0.0 for the other slots, which changes no bit): no hand-off.
+  if (ns == 1 || sg.pad == 0) {
     const double y = 0.0 + p;
     if (A.long_defer) {
       A.ypart[sg.ri] = y;
@@ -661,22 +664,23 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
     return;
   }
   // Hand-off (MI355X_MICROARCH.md, valid forms, first table row): publish the piece sum
-  // write-through (sc1), drain this wave's stores, then ONE agent-scope atomic add on the
-  // row's arrival counter; the publisher whose add returns the row's last count (mod S:
-  // the counter runs on across launches, S divides 2^32) is the only one that reads the
-  // S slots (sc1 loads, after its add has returned) and finalises the row. The atomic
-  // adds of a row are totally ordered at the memory side, so exactly one publisher per
-  // launch sees the last count and every slot it reads was drained before the add that
-  // preceded its own. No thread ever waits on another: nothing depends on dispatch order.
+  // write-through (sc1), drain this wave's stores, then ONE agent-scope atomic increment
+  // of the row's arrival counter, wrapping at the row's piece count (atomic_inc: old >=
+  // pad ? 0 : old + 1, so the counter runs on across launches); the publisher whose
+  // increment returns pad (the row's last arrival) is the only one that reads the S slots
+  // (sc1 loads, after its increment has returned) and finalises the row. The atomics of a
+  // row are totally ordered at the memory side, so exactly one publisher per launch sees
+  // the last count and every slot it reads was drained before the atomic that preceded
+  // its own. No thread ever waits on another: nothing depends on dispatch order.
   unsigned long long* slots = reinterpret_cast<unsigned long long*>(A.P + (size_t)sg.ri * kSlotStride);
   __hip_atomic_store(slots + s, (unsigned long long)__double_as_longlong(p), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   TPL_MARK(4);
-  const unsigned int arrived = __hip_atomic_fetch_add(A.Pcnt + (size_t)sg.ri * kCntStride, 1u,
-                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  asm volatile("" ::: "memory");  // the slot loads stay behind the returned add
-  if ((arrived & (unsigned)(ns - 1)) != (unsigned)(ns - 1)) return;
+  const unsigned int arrived = __builtin_amdgcn_atomic_inc32(
+      A.Pcnt + (size_t)sg.ri * kCntStride, (unsigned)sg.pad, __ATOMIC_RELAXED, "agent");
+  asm volatile("" ::: "memory");  // the slot loads stay behind the returned increment
+  if (arrived != (unsigned)sg.pad) return;
   // 16-B sc1 loads of slot pairs (slot arrays are 64-B aligned): four instead of eight 8-B
   // loads (same box, alternated: k_p2_spmv -0.1 us, pass one -0.15 us per step). The four
   // loads and their wait are ONE asm statement: the compiler must not touch the destination

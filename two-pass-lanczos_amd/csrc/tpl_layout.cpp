@@ -178,10 +178,21 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   std::unordered_set<int64_t> lines;  // distinct 128-B lines of the open bin (bin_lines)
   const int segs = sp.bin_segs > 0 && sp.bin_segs < kBinSegs ? sp.bin_segs : kBinSegs;
   std::vector<int64_t> plines;
+  // Only the pieces with entries are packed (a row's empty pieces would only publish
+  // +0.0, which its never-written slot already holds; a row with no entries at all keeps
+  // its slice-0 piece); pieces_of[r] = the row's packed pieces, its arrival count.
+  std::vector<int32_t> pieces_of(nlb, 0);
+  for (size_t r = 0; r < nlb; ++r) {
+    for (int s = 0; s < S; ++s)
+      pieces_of[r] += poff[r * (S + 1) + s + 1] > poff[r * (S + 1) + s];
+    pieces_of[r] = std::max(pieces_of[r], 1);
+  }
   for (int s = 0; s < S && nlb > 0; ++s) {
     lines.clear();
     for (size_t r = 0; r < nlb; ++r) {
       const int32_t cnt = poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
+      if (cnt == 0 && !(s == 0 && pieces_of[r] == 1 && poff[r * (S + 1) + S] == poff[r * (S + 1)]))
+        continue;
       bool over = false;
       if (sp.bin_lines > 0) {
         plines.clear();
@@ -236,7 +247,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
         for (size_t j = 0; j < pieces.size(); ++j) {
           const int32_t r = pieces[j].first, start = pieces[j].second;
           const int32_t q0 = poff[r * (S + 1) + s], q1 = poff[r * (S + 1) + s + 1];
-          L.b_seg[bin * kTPB + j] = BinSeg{start, r, L.lrows[r], 0};
+          L.b_seg[bin * kTPB + j] = BinSeg{start, r, L.lrows[r], pieces_of[r] - 1};
           for (int32_t q = q0; q < q1; ++q) {
             L.b_col[bin * L.bin_cap + start + (q - q0)] = cmap(col[q]);
             L.b_val[bin * L.bin_cap + start + (q - q0)] = val[q];
