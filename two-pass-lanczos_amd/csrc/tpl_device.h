@@ -13,8 +13,9 @@
 //     computed, not loaded, and the kernel is specialised for W.
 //   * LONG rows are cut into S column slices [floor(n*s/S), floor(n*(s+1)/S)), S in
 //     {1, 2, 4, 8} (tpl_runtime.cpp auto_slices: the fewest whose share of the
-//     gathered vector fits an eighth of an L2). The (row, slice) pieces of slice s, long
-//     rows ascending, are packed whole into BINS of bin_cap entries (padding
+//     gathered vector fits an eighth of an L2). The (row, slice) pieces of slice s that
+//     hold entries (a row with none keeps its slice-0 piece), long rows ascending, are
+//     packed whole into BINS of bin_cap entries (padding
 //     col = -1) with at most kBinSegs pieces each; every slice gets the same number
 //     M of bins. Bin m of slice s is workgroup S*m + s of the slice part of the
 //     grid: under the round-robin dispatch of workgroups to XCDs the bins of a slice
@@ -22,11 +23,13 @@
 //     only, never correctness). A bin's entries are read at computed addresses
 //     (thread t: entries t + 256u), the products are staged in LDS, and each piece
 //     is summed by 8 lanes (by a whole wave when longer than kBigPiece; those
-//     pieces lead the table). With S = 1 a piece is its whole row, finished in
-//     place. Otherwise every piece sum is published write-through into the row's
-//     slot; after its store drains, the publisher adds 1 to the row's arrival counter
-//     (agent-scope atomic), and the one whose add returns the row's last count reads
-//     the S slots and finalises the row (sums the slots, runs the epilogue).
+//     pieces lead the table). A row with one packed piece (always with S = 1) is
+//     finished in place by that piece's thread. Otherwise every piece sum is published
+//     write-through into the row's slot (the slots of unpacked pieces are never written:
+//     they hold the +0.0 an empty piece sums to); after its store drains, the publisher
+//     increments the row's arrival counter (agent-scope atomic_inc wrapping at the row's
+//     packed-piece count, BinSeg::pad), and the one whose increment returns the row's last
+//     count reads the S slots and finalises the row (sums the slots, runs the epilogue).
 //     Nobody waits on anybody.
 //
 // Canonical reduction order (reproduced bit for bit by oracle/lanczos_oracle.c):
@@ -102,11 +105,12 @@ constexpr int kWinMax = 2048;        // short-chunk column window in LDS: at mos
 constexpr int kWinLoads = kWinMax / 256;  // window loads per thread
 constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
 // Arrival counters of the sliced long rows: one uint32 per row, kCntStride apart (one
-// 64-B segment each, so the adds of different rows never share a segment).
+// 64-B segment each, so the atomics of different rows never share a segment).
 constexpr int kCntStride = 16;
 constexpr double kBreakdownTol = 2.220446049250313080847263336181640625e-13; // 1000*f64::EPSILON, src/algorithms/mod.rs:140-143
 
-// One bin-table slot: piece start (offset in the bin), long-row index, global row.
+// One bin-table slot: piece start (offset in the bin), long-row index, global row, and
+// the row's packed pieces - 1 (its last arrival count; 0: the piece is the whole row).
 // Slot j < pieces describes piece j (its end is slot j+1's start); the slot after
 // the last piece holds the bin's fill with ri = row = -1, and so do all later slots.
 // x terms pass-two step j (1 .. last) applies (EpiPass2): the terms pending since the
