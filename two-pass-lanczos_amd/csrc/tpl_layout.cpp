@@ -187,6 +187,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
       pieces_of[r] += poff[r * (S + 1) + s + 1] > poff[r * (S + 1) + s];
     pieces_of[r] = std::max(pieces_of[r], 1);
   }
+  int nbig_open = 0, nsmall_open = 0;  // the open bin's long / other pieces
   for (int s = 0; s < S && nlb > 0; ++s) {
     lines.clear();
     for (size_t r = 0; r < nlb; ++r) {
@@ -202,10 +203,14 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
         plines.erase(std::unique(plines.begin(), plines.end()), plines.end());
         over = !lines.empty() && lines.size() + plines.size() > (size_t)sp.bin_lines;
       }
+      const bool big = cnt > kBigPiece;
       if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
-          (int)bins[s].back().size() == segs || over) {
+          (int)bins[s].back().size() == segs || over ||
+          (big && sp.bin_big > 0 && nbig_open == sp.bin_big) ||
+          (!big && sp.bin_small > 0 && nsmall_open == sp.bin_small)) {
         bins[s].emplace_back();
         fill[s].push_back(0);
+        nbig_open = nsmall_open = 0;
         lines.clear();
         if (sp.bin_lines > 0) {  // recount the piece against the empty bin
           plines.clear();
@@ -216,6 +221,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
       lines.insert(plines.begin(), plines.end());
       bins[s].back().emplace_back((int32_t)r, fill[s].back());
       fill[s].back() += cnt;
+      (big ? nbig_open : nsmall_open)++;
     }
   }
   L.M = 0;

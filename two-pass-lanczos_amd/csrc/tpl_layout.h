@@ -24,6 +24,10 @@ struct SchedParams {
   int bin_lines = 0;                // > 0: also close a bin once its gathers would touch
                                     // more than this many distinct 128-B lines (lab)
   int bin_segs = 0;                 // > 0: at most this many pieces per bin (0: kBinSegs)
+  int bin_big = 0;                  // > 0: at most this many pieces longer than kBigPiece
+                                    // per bin (their 16-lane sums run kTPB / 16 per pass)
+  int bin_small = 0;                // > 0: at most this many other pieces per bin (their
+                                    // 8-lane sums run kTPB / 8 per pass)
 };
 
 // Host copy of the SpMV layout (tpl_device.h).

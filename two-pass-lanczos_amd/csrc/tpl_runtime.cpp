@@ -378,6 +378,8 @@ void rebuild_schedule(tpl_op_s* op) {
   if (const char* e = std::getenv("TPL_ELEM_ROWS")) sp.elem_rows = std::atoi(e);
   if (const char* e = std::getenv("TPL_BIN_LINES")) sp.bin_lines = std::atoi(e);
   if (const char* e = std::getenv("TPL_BIN_SEGS")) sp.bin_segs = std::atoi(e);
+  if (const char* e = std::getenv("TPL_BIN_BIG")) sp.bin_big = std::atoi(e);
+  if (const char* e = std::getenv("TPL_BIN_SMALL")) sp.bin_small = std::atoi(e);
   if (const char* e = std::getenv("TPL_SLICES")) {  // auto slice count only; the values
     const int s = std::atoi(e);                     // tpl_op_set_slices accepts
     if (sp.slices <= 0 && s > 0 && s <= kSlices && (s & (s - 1)) == 0) sp.slices = s;
