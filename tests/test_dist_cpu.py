@@ -13,7 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 sys.path.insert(0, os.path.join(os.path.dirname(HERE), "two-pass-lanczos_amd"))
 
-from conftest import harness_b, load_kkt  # noqa: E402
+from conftest import banded_hub, harness_b, load_kkt  # noqa: E402
 
 
 def _free_port():
@@ -43,7 +43,7 @@ def test_partition_errors():
         partition((2, np.array([0, 1, 2]), np.array([0, 1]), np.ones(2)), 3)
 
 
-def _worker(rank, world, port, tmp, arcs):
+def _worker(rank, world, port, tmp, arcs, halo=False):
     import torch.distributed as tdist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     tdist.init_process_group("gloo", rank=rank, world_size=world)
@@ -55,19 +55,25 @@ def _worker(rank, world, port, tmp, arcs):
         a = load_kkt(arcs, tmp).a
         b = harness_b(a)
         st = partition(a, world)
-        x, al, be = dist_sim.two_pass(tdist, rank, world, a, st, b, 50, ftk_ref.inv)
-        np.savez(os.path.join(tmp, f"rank{rank}.npz"), x=x, al=al, be=be, st=st)
+        x, al, be = dist_sim.two_pass(tdist, rank, world, a, st, b, 50, ftk_ref.inv, halo=halo)
+        np.savez(os.path.join(tmp, f"{'halo' if halo else 'rows'}{rank}.npz"), x=x, al=al, be=be,
+                 st=st)
     finally:
         tdist.destroy_process_group()
 
 
-def test_dist_protocol_two_ranks(kkt_tmp):
+@pytest.mark.parametrize("halo", [False, True])
+def test_dist_protocol_two_ranks(kkt_tmp, halo):
+    """The row-block exchange (whole vector all-gathered) and the halo exchange
+    (tpl_dist_op_create_halo: only the referenced rows, packed into per-rank slots; NaN
+    anywhere else) over gloo, world 2, against the single-process oracle."""
     import torch.multiprocessing as mp
     import oracle
     from oracle import ftk_ref
     world = 2
-    mp.spawn(_worker, args=(world, _free_port(), kkt_tmp, 5000), nprocs=world, join=True)
-    r = [np.load(os.path.join(kkt_tmp, f"rank{i}.npz")) for i in range(world)]
+    mp.spawn(_worker, args=(world, _free_port(), kkt_tmp, 5000, halo), nprocs=world, join=True)
+    r = [np.load(os.path.join(kkt_tmp, f"{'halo' if halo else 'rows'}{i}.npz"))
+         for i in range(world)]
     # identical coefficients on every rank
     assert np.array_equal(r[0]["al"], r[1]["al"]) and np.array_equal(r[0]["be"], r[1]["be"])
     x = np.concatenate([r[i]["x"] for i in range(world)])
@@ -75,6 +81,45 @@ def test_dist_protocol_two_ranks(kkt_tmp):
     b = harness_b(a)
     xo = oracle.Operator(a).lanczos_two_pass(b, 50, ftk_ref.inv)
     assert np.linalg.norm(x - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
+def _banded_worker(rank, world, port, tmp, halo):
+    import torch.distributed as tdist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    tdist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sys.path.insert(0, HERE)
+        import dist_sim
+        from tpl_amd.dist import partition
+        from oracle import ftk_ref
+        a = banded_hub(n=3000, hub_every=499)
+        st = partition(a, world)
+        x, al, be = dist_sim.two_pass(tdist, rank, world, a, st, harness_b(a), 30, ftk_ref.inv,
+                                      halo=halo)
+        np.savez(os.path.join(tmp, f"banded_{int(halo)}_{rank}.npz"), x=x, al=al, be=be)
+    finally:
+        tdist.destroy_process_group()
+
+
+def test_halo_protocol_banded_three_ranks(tmp_path):
+    """World 3 over gloo on a matrix without the KKT structure (band + long hub rows): the
+    halo exchange gives the row-block exchange's bits (the same arithmetic, only the
+    referenced rows moved) and agrees with the single-process oracle."""
+    import torch.multiprocessing as mp
+    import oracle
+    from oracle import ftk_ref
+    world = 3
+    res = {}
+    for halo in (False, True):
+        mp.spawn(_banded_worker, args=(world, _free_port(), str(tmp_path), halo), nprocs=world,
+                 join=True)
+        r = [np.load(os.path.join(tmp_path, f"banded_{int(halo)}_{i}.npz")) for i in range(world)]
+        res[halo] = (np.concatenate([q["x"] for q in r]), r[0]["al"], r[0]["be"])
+    for u, v in zip(res[False], res[True]):
+        assert np.array_equal(u, v)
+    a = banded_hub(n=3000, hub_every=499)
+    xo = oracle.Operator(a).lanczos_two_pass(harness_b(a), 30, ftk_ref.inv)
+    assert np.linalg.norm(res[True][0] - xo) <= 1e-12 * np.linalg.norm(xo)
 
 
 def _plan_worker(rank, world, port, tmp, arcs, mode):
