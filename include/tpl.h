@@ -347,8 +347,9 @@ tpl_status tpl_op_step_samples(tpl_op_t op, double* p1_spmv_us, double* p1_axpy_
 
 /* ---- row-partitioned operator over several GPUs ----------
  * One process per GPU. Rank r holds the rows [starts[r], starts[r+1]) of A; every
- * SpMV gathers the full vector with an in-place all-gather (RCCL over xGMI), and
- * alpha / beta combine the ranks' totals (each rank reduces its own partials in the
+ * SpMV gathers the full vector with an in-place all-gather (RCCL over xGMI) — or only
+ * its halo (tpl_dist_op_create_halo), or, with replicated long rows, their partials
+ * (tpl_dist_op_create_replicated) — and alpha / beta combine the ranks' totals (each rank reduces its own partials in the
  * single-GPU canonical order; the R totals are all-gathered and reduced in rank
  * order), so all ranks hold bitwise identical alpha, beta and steps. The solver
  * entry points above take a partitioned operator unchanged; b, x_out and v_out are
