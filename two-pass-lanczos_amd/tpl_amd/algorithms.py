@@ -28,7 +28,7 @@ import numpy as np
 
 from . import _lib
 from ._vec import Vec
-from .error import LanczosError, check
+from .error import check
 from .operator import HipCsrOp
 
 BREAKDOWN_TOLERANCE = 1000.0 * np.finfo(np.float64).eps  # src/algorithms/mod.rs:140-143
