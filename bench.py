@@ -341,12 +341,21 @@ def predicted_block(world: int, k: int, steps: int, solve_s: float):
     c = 2 * steps + (steps - 1)
     # the N-rank solve runs at the pace of its slowest rank's share
     t0 = max(sh.get("ms_per_solve_every_rank") or [one["ms_per_solve"]])
+    kern = None
+    try:  # the per-step kernels of the share (rocprofv3 trace medians; N = 8 only)
+        with open(os.path.join(ROOT, "profiles", f"rank_share_n{world}_kernels.json")) as f:
+            kern = json.load(f)
+    except (OSError, ValueError):
+        pass
     return {"source": f"profiles/rank_share.json ({rs.get('source', 'scripts/rank_share.py')})",
             "rank0_rows": sh["rank0_rows"], "rank0_nnz": sh["rank0_nnz"],
             "ms_every_rank_share": sh.get("ms_per_solve_every_rank"),
             "per_step_us_1rank": {"pass1": one["pass1_us_per_step"],
                                   "pass2": one["pass2_us_per_step"]},
             "exchange_1rank_us": one.get("exchange_1rank_us"),
+            "per_step_kernels_trace_us": None if kern is None else {
+                "pass1": kern.get("pass1_step"), "pass2": kern.get("pass2_step"),
+                "source": f"profiles/rank_share_n{world}_kernels.json", "note": kern.get("note")},
             "single_gpu_same_share_ms": sh.get("single_gpu", {}).get("ms_per_solve"),
             "collectives_per_step": sh["collectives_per_step"], "collectives_per_solve": c,
             "model": "ms = slowest rank's share (ms_1rank) + collectives_per_solve * L / 1000",

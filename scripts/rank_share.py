@@ -41,6 +41,9 @@ def main():
     ap.add_argument("--all-ranks", type=int, default=1,
                     help="1: every rank's share (the N-rank solve waits for the slowest); "
                          "0: rank 0's only")
+    ap.add_argument("--single", type=int, default=1,
+                    help="1: also solve rank 0's share on the single-GPU path (0: the "
+                         "one-rank partition only, e.g. under rocprofv3)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rank_share.json"))
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -58,7 +61,7 @@ def main():
     ctx = DistContext(0, 1, device=0, transport="rccl")
     out = {"workload": f"configs[4]: {data}", "k": args.k, "shares": {}}
     for N in args.ranks:
-        res = share(a, N, 0, args, ctx)
+        res = share(a, N, 0, args, ctx, single=bool(args.single))
         if args.all_ranks and N > 1:
             # every other rank's share through one RCCL rank (its kernels only): the N-rank
             # solve runs at the pace of the slowest
