@@ -110,6 +110,16 @@ def banded_hub(n=20000, w=3, hub_every=997, hub_half=150, hub_step=7, seed=5):
     return a
 
 
+def block_diag_spd(blocks=3, m=1500, seed=7):
+    """blocks independent SPD blocks of m rows (band + a long row each): a partition at
+    the block boundaries needs no halo at all."""
+    import scipy.sparse as sp
+    parts = [banded_hub(n=m, hub_every=m // 3, seed=seed + i) for i in range(blocks)]
+    a = sp.block_diag(parts).tocsr()
+    a.sort_indices()
+    return a
+
+
 def harness_b(a):
     """b = A (1/sqrt(n)) 1, as src/bin/tradeoff.rs:235-236 (row-sequential sums)."""
     n = a.shape[0]

@@ -21,12 +21,17 @@ def main():
     tdist.init_process_group("gloo", rank=rank, world_size=world)
     import tpl_amd
     from tpl_amd.dist import DistContext, DistHipCsrOp
-    from conftest import banded_hub, harness_b, load_kkt
-    # TPL_TEST_MATRIX=banded: tests/conftest.py banded_hub (no KKT structure) instead
-    a = banded_hub() if os.environ.get("TPL_TEST_MATRIX") == "banded" else load_kkt(arcs, out).a
+    from conftest import banded_hub, block_diag_spd, harness_b, load_kkt
+    # TPL_TEST_MATRIX=banded / blockdiag: tests/conftest.py banded_hub / block_diag_spd (no
+    # KKT structure) instead; TPL_TEST_STARTS: the row split ("0,1500,...")
+    kind = os.environ.get("TPL_TEST_MATRIX")
+    a = (banded_hub() if kind == "banded" else block_diag_spd() if kind == "blockdiag"
+         else load_kkt(arcs, out).a)
+    st = os.environ.get("TPL_TEST_STARTS")
+    starts = None if not st else np.array([int(v) for v in st.split(",")], dtype=np.int64)
     b = harness_b(a)
     ctx = DistContext(rank, world, device=int(os.environ.get("TPL_DEVICE", "0")), transport=transport)
-    op = DistHipCsrOp(a, ctx, mode=mode)
+    op = DistHipCsrOp(a, ctx, starts=starts, mode=mode)
     if os.environ.get("TPL_TEST_SLICES"):  # diagnostics: force the long-row slice count
         op.set_slices(int(os.environ["TPL_TEST_SLICES"]))
     bl = op.local(b)

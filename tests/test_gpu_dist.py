@@ -199,3 +199,29 @@ def test_halo_banded_host_transport(tmp_path, world):
     y = _assemble(halo, "y", a.shape[0])
     yr = a @ np.cos(np.arange(a.shape[0]))
     np.testing.assert_allclose(y, yr, rtol=1e-12, atol=1e-12)
+
+
+def test_halo_without_halo_host_transport(tmp_path):
+    """Three independent blocks split at their boundaries (TPL_TEST_STARTS): the halo is
+    empty, so no rank packs or exchanges a vector part (pass two moves 0 bytes per step,
+    pass one only the two totals) — and the bits are still the plain row blocks' (which
+    all-gather every block) and the restated partitioned order's."""
+    from conftest import block_diag_spd
+    env = {"TPL_TEST_MATRIX": "blockdiag", "TPL_TEST_STARTS": "0,1500,3000,4500"}
+    a = block_diag_spd()
+    rows = _run_ranks(str(tmp_path / "rows"), 3, "host", mode="rows", extra_env=env)
+    halo = _run_ranks(str(tmp_path / "halo"), 3, "host", mode="halo", extra_env=env)
+    for rr, rh in zip(rows, halo):
+        assert str(rh["mode"]) == "halo"
+        assert np.array_equal(rh["starts"], [0, 1500, 3000, 4500])
+        for key in ("rows", "x1", "x2", "x3", "xs", "al", "be", "y"):
+            assert np.array_equal(rr[key], rh[key]), key
+        assert list(rh["ex_bytes"]) == [8 * 3 * 2, 0]
+    from partition_oracle import PartitionOracle
+    import tpl_amd
+    po = PartitionOracle(a, halo, "rows")
+    b = harness_b(a)
+    al, be, s, bn = po.pass_one(b, 50)
+    assert np.array_equal(halo[0]["al"], al) and np.array_equal(halo[0]["be"], be)
+    xo = po.pass_two(b, al, be, s, bn, tpl_amd.ftk.INV(al, be) * bn)
+    assert np.array_equal(_assemble(halo, "x1", a.shape[0]), xo)
