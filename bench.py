@@ -1113,6 +1113,15 @@ def main():
             "loadavg_before_after": [round(load0[0], 2), round(load1[0], 2)],
             "compiler": ORACLE_CFLAGS, **host_info()}
         out["speedup_vs_cpu"] = round(value / (kc / tc), 1)
+        if (arcs, args.k, args.f) == (500000, 500, "inv"):
+            # context only (not vs_baseline: BASELINE.md publishes times, not this metric):
+            # the reference's own CPU times for this solve on its Xeon, one thread
+            out["reference_published_cpu"] = {
+                "two_pass_k500_s": {"results/tradeoff_arcs500k_rho3.csv:31": 7.539755,
+                                    "results/scalability_k500_rho3.csv:21": 5.27505},
+                "derived_iterations_per_s": [66.3, 94.8],
+                "ratio_of_value": [round(value / 66.3, 1), round(value / 94.8, 1)],
+                "hardware": "2x Xeon Gold 5318Y, parallelism disabled (BASELINE.md)"}
         if exp_case is not None:
             # configs[1]: the device exp is held to a tolerance (an EVD-class evaluation,
             # not the host QL's bits): x against the reference-order oracle with LAPACK's
