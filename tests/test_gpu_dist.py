@@ -225,3 +225,44 @@ def test_halo_without_halo_host_transport(tmp_path):
     assert np.array_equal(halo[0]["al"], al) and np.array_equal(halo[0]["be"], be)
     xo = po.pass_two(b, al, be, s, bn, tpl_amd.ftk.INV(al, be) * bn)
     assert np.array_equal(_assemble(halo, "x1", a.shape[0]), xo)
+
+
+def test_halo_create_rejects_bad_input():
+    """tpl_dist_op_create_halo validates before touching the device: a non-increasing or
+    short split, fewer rows than ranks and unsorted columns are refused with
+    TPL_ERR_INVALID_ARGUMENT and no operator (rank 0 of a two-rank host transport whose
+    exchange is never called)."""
+    from ctypes import POINTER, byref, c_double, c_int32, c_int64, c_void_p
+
+    import scipy.sparse as sp
+    from tpl_amd import _lib
+
+    cb = _lib.ALLGATHER_FN(lambda *args: 1)
+    d = c_void_p()
+    assert _lib.tpl_dist_create_host(0, 0, 2, cb, None, byref(d)) == _lib.TPL_OK
+    try:
+        a = sp.identity(6, format="csr") * 2.0
+        rp = np.ascontiguousarray(a.indptr, dtype=np.int64)
+        ci = np.ascontiguousarray(a.indices, dtype=np.int32)
+        v = np.ascontiguousarray(a.data, dtype=np.float64)
+
+        def create(n, starts, rp=rp, ci=ci):
+            h = c_void_p()
+            st = None if starts is None else np.ascontiguousarray(starts, dtype=np.int64)
+            s = _lib.tpl_dist_op_create_halo(
+                d.value, n, None if st is None else st.ctypes.data_as(POINTER(c_int64)),
+                rp.ctypes.data_as(POINTER(c_int64)), ci.ctypes.data_as(POINTER(c_int32)),
+                v.ctypes.data_as(POINTER(c_double)), byref(h))
+            if s == _lib.TPL_OK:
+                _lib.tpl_op_destroy(h.value)
+            return s, h.value
+
+        assert create(6, [0, 4, 3]) == (_lib.TPL_ERR_INVALID_ARGUMENT, None)  # unordered
+        assert create(6, [0, 3, 5]) == (_lib.TPL_ERR_INVALID_ARGUMENT, None)  # short
+        assert create(1, None, rp=rp[:2]) == (_lib.TPL_ERR_INVALID_ARGUMENT, None)  # 1 row, 2 ranks
+        bad = ci.copy()
+        bad[0] = 7  # column out of range
+        assert create(6, None, ci=bad)[0] == _lib.TPL_ERR_INVALID_ARGUMENT
+        assert create(6, [0, 3, 6])[0] == _lib.TPL_OK
+    finally:
+        _lib.tpl_dist_destroy(d.value)
