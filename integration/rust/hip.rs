@@ -31,6 +31,14 @@
 //! `stack` is accepted and left untouched: the engine keeps its workspace in HBM
 //! (faer's `apply_scratch` of [`HipCsrOp`] is empty for the same reason).
 //!
+//! Several GPUs (an extension: the reference is single-threaded, `Par::Seq`): one process
+//! per GPU, each creates a [`HipDist`] (the RCCL communicator; rank 0's
+//! [`HipDist::unique_id`] bytes reach the others by any channel the host program has —
+//! MPI, a file, a socket) and then [`HipCsrOp::partitioned`] from the SAME whole matrix.
+//! The functions below take the partitioned operator unchanged; `b` and the returned `x`
+//! (and V_k) are then this rank's rows, [`HipCsrOp::local_rows`] — the same contract as
+//! include/tpl.h's row-partitioned operators.
+//!
 //! Written against faer 0.22.6 (the reference's Cargo.toml). This image has no Rust
 //! toolchain, so the file is UNCOMPILED here; tests/test_boundary.py type-checks every
 //! `extern "C"` item, both callback types and the `#[repr(C)]` struct against
@@ -59,6 +67,12 @@ pub struct TplCtx {
 pub struct TplOp {
     _p: [u8; 0],
 }
+#[repr(C)]
+pub struct TplDist {
+    _p: [u8; 0],
+}
+/// TPL_DIST_ID_BYTES (include/tpl.h): the RCCL unique id rank 0 creates.
+pub const TPL_DIST_ID_BYTES: usize = 128;
 /// `tpl_ftk_fn` (include/tpl.h): the `f_tk_solver` closure behind a C callback.
 type FtkFn = unsafe extern "C" fn(*const f64, usize, *const f64, usize, *mut f64, usize,
                                   *mut usize, *mut c_char, usize, *mut c_void) -> c_int;
@@ -106,6 +120,18 @@ extern "C" {
                             b_norm: f64, y: *const f64, y_len: usize, x_out: *mut f64,
                             v_out: *mut f64, mem: c_int) -> c_int;
     fn tpl_copy_to_host(dst: *mut c_void, src_device: *const c_void, bytes: usize) -> c_int;
+    fn tpl_op_nrows(op: *mut TplOp) -> i64;
+    fn tpl_op_local_rows(op: *mut TplOp, rows: *mut i64) -> c_int;
+    fn tpl_dist_unique_id(id: *mut u8) -> c_int;
+    fn tpl_dist_create(device: c_int, rank: c_int, nranks: c_int, id: *const u8,
+                       out: *mut *mut TplDist) -> c_int;
+    fn tpl_dist_destroy(d: *mut TplDist) -> c_int;
+    fn tpl_dist_op_create_replicated(d: *mut TplDist, n: i64, row_ptr: *const i64,
+                                     col_idx: *const i32, vals: *const f64,
+                                     out: *mut *mut TplOp) -> c_int;
+    fn tpl_dist_op_create_halo(d: *mut TplDist, n: i64, starts: *const i64,
+                               row_ptr: *const i64, col_idx: *const i32, vals: *const f64,
+                               out: *mut *mut TplOp) -> c_int;
 }
 
 fn cstr(p: *const c_char) -> String {
@@ -154,10 +180,13 @@ fn check(st: c_int) -> Result<(), LanczosError> {
 pub struct HipCsrOp {
     ctx: *mut TplCtx,
     op: *mut TplOp,
+    /// this operator's rows: all of A, or this rank's part of a partitioned A
     n: usize,
     /// One engine call at a time per operator (include/tpl.h: not re-entrant); this is
     /// what makes the operator `Sync`, as faer's `LinOp` requires.
     lock: Mutex<()>,
+    /// partitioned: the communicator, kept alive until the operator is destroyed
+    dist: Option<std::sync::Arc<HipDist>>,
 }
 
 // SAFETY: the handles are only used under `lock`, and the engine's per-thread error
@@ -212,7 +241,56 @@ impl HipCsrOp {
                 return Err(e);
             }
         }
-        Ok(Self { ctx, op, n, lock: Mutex::new(()) })
+        Ok(Self { ctx, op, n, lock: Mutex::new(()), dist: None })
+    }
+
+    /// This rank's part of the symmetric `a` over `dist`'s ranks (every rank passes the
+    /// same whole matrix; collective: all ranks make the same calls in the same order).
+    /// `Partition::Replicated` (the KKT form: tpl_dist_op_create_replicated, refused with
+    /// a SolverError when a short row references another rank's short rows),
+    /// `Partition::Halo` (any symmetric matrix: tpl_dist_op_create_halo over the
+    /// byte-balanced row blocks), `Partition::Auto` (replicated when it applies, else
+    /// halo).
+    pub fn partitioned(a: SparseColMatRef<'_, usize, f64>, dist: &std::sync::Arc<HipDist>,
+                       partition: Partition) -> Result<Self, LanczosError> {
+        if a.nrows() != a.ncols() {
+            return Err(LanczosError(LanczosErrorKind::DimensionMismatch {
+                operator_cols: a.ncols(),
+                vector_rows: a.nrows(),
+            }));
+        }
+        let (rp, ci, v) = compact_arrays(a);
+        let n = a.nrows() as i64;
+        let mut op = std::ptr::null_mut();
+        const TPL_ERR_UNSUPPORTED: c_int = 104; // the matrix does not allow the split
+        unsafe {
+            let mut replicated = false;
+            if partition != Partition::Halo {
+                let st = tpl_dist_op_create_replicated(dist.d, n, rp.as_ptr(), ci.as_ptr(),
+                                                       v.as_ptr(), &mut op);
+                if st != 0 && (partition == Partition::Replicated || st != TPL_ERR_UNSUPPORTED) {
+                    check(st)?;
+                }
+                replicated = st == 0;
+            }
+            if !replicated {
+                check(tpl_dist_op_create_halo(dist.d, n, std::ptr::null(), rp.as_ptr(),
+                                              ci.as_ptr(), v.as_ptr(), &mut op))?;
+            }
+            let nl = tpl_op_nrows(op) as usize;
+            Ok(Self { ctx: std::ptr::null_mut(), op, n: nl, lock: Mutex::new(()),
+                      dist: Some(dist.clone()) })
+        }
+    }
+
+    /// The global row of each entry of this operator's vectors (`b` and `x` of the
+    /// functions below hold these rows, in this order).
+    pub fn local_rows(&self) -> Result<Vec<i64>, LanczosError> {
+        let mut rows = vec![0i64; self.n.max(1)];
+        let _g = self.lock.lock().unwrap();
+        unsafe { check(tpl_op_local_rows(self.op, rows.as_mut_ptr()))? };
+        rows.truncate(self.n);
+        Ok(rows)
     }
 
     pub fn nrows(&self) -> usize {
@@ -232,7 +310,53 @@ impl Drop for HipCsrOp {
     fn drop(&mut self) {
         unsafe {
             tpl_op_destroy(self.op);
-            tpl_ctx_destroy(self.ctx);
+            if !self.ctx.is_null() {
+                tpl_ctx_destroy(self.ctx);
+            }
+        }
+        // `dist` (the communicator) is released after the operator, when its field drops
+    }
+}
+
+/// How [`HipCsrOp::partitioned`] splits the matrix over the ranks (include/tpl.h).
+#[derive(Clone, Copy, Debug, PartialEq, Eq)]
+pub enum Partition {
+    Replicated,
+    Halo,
+    Auto,
+}
+
+/// One rank's RCCL communicator over xGMI (tpl_dist_create).
+pub struct HipDist {
+    d: *mut TplDist,
+}
+
+// SAFETY: the communicator is only used by the operators built on it, each under its own
+// lock; the engine serialises the collectives on the operator's stream.
+unsafe impl Send for HipDist {}
+unsafe impl Sync for HipDist {}
+
+impl HipDist {
+    /// Rank 0: the id every rank passes to [`HipDist::new`].
+    pub fn unique_id() -> Result<[u8; TPL_DIST_ID_BYTES], LanczosError> {
+        let mut id = [0u8; TPL_DIST_ID_BYTES];
+        unsafe { check(tpl_dist_unique_id(id.as_mut_ptr()))? };
+        Ok(id)
+    }
+
+    /// This process's rank of `nranks` on GPU `device` (collective over the ranks).
+    pub fn new(device: i32, rank: i32, nranks: i32, id: &[u8; TPL_DIST_ID_BYTES])
+               -> Result<std::sync::Arc<Self>, LanczosError> {
+        let mut d = std::ptr::null_mut();
+        unsafe { check(tpl_dist_create(device, rank, nranks, id.as_ptr(), &mut d))? };
+        Ok(std::sync::Arc::new(Self { d }))
+    }
+}
+
+impl Drop for HipDist {
+    fn drop(&mut self) {
+        unsafe {
+            tpl_dist_destroy(self.d);
         }
     }
 }
@@ -240,6 +364,7 @@ impl Drop for HipCsrOp {
 /// faer's `LinOp<f64>` over `tpl_op_apply`: a compatibility path, so the reference's own
 /// generic code (e.g. `solvers::lanczos` itself) can run with the product on the GPU. The
 /// solvers of this module never use it — they hand the whole recurrence to the engine.
+/// (For a partitioned operator it is this rank's block of rows, a collective call.)
 impl LinOp<f64> for HipCsrOp {
     fn apply_scratch(&self, _rhs_ncols: usize, _par: Par) -> StackReq {
         StackReq::EMPTY // the engine's workspace lives in HBM

@@ -246,7 +246,7 @@ REF_SRC = "/root/reference/src"
 _C_TO_RUST = {"double": "f64", "int": "c_int", "int32_t": "i32", "int64_t": "i64",
               "uint64_t": "u64", "uint8_t": "u8", "size_t": "usize", "char": "c_char",
               "void": "c_void", "tpl_status": "c_int", "tpl_ctx_t": "*mut TplCtx",
-              "tpl_op_t": "*mut TplOp", "tpl_ftk_fn": "FtkFn",
+              "tpl_op_t": "*mut TplOp", "tpl_dist_t": "*mut TplDist", "tpl_ftk_fn": "FtkFn",
               # the step callback is optional (NULL = none): a nullable fn pointer
               "tpl_step_cb": "Option<StepCb>", "tpl_error_detail": "TplErrorDetail"}
 
