@@ -329,6 +329,14 @@ def test_rust_shim_extern_types_match_header():
     # the ones VERDICT r04 found missing
     names = {m.group(1) for m in items}
     assert {"tpl_lanczos_standard", "tpl_copy_to_host", "tpl_lanczos_pass_two"} <= names
+    # the multi-GPU operators (HipDist, HipCsrOp::partitioned)
+    assert {"tpl_dist_unique_id", "tpl_dist_create", "tpl_dist_destroy",
+            "tpl_dist_op_create_replicated", "tpl_dist_op_create_halo",
+            "tpl_op_local_rows", "tpl_op_nrows"} <= names
+    src, _ = _extern_block()
+    for item in ("pub struct HipDist", "pub fn partitioned", "pub fn local_rows",
+                 "pub enum Partition", "pub fn unique_id"):
+        assert item in src, item
 
 
 def test_rust_shim_callback_and_struct_types_match_header():
