@@ -24,6 +24,7 @@
 #define TPL_HPP_
 
 #include <algorithm>
+#include <array>
 #include <cstdint>
 #include <cstring>
 #include <exception>
@@ -219,6 +220,36 @@ class Context {
   tpl_ctx_t ctx_ = nullptr;
 };
 
+// One rank's RCCL communicator over xGMI (tpl_dist_create), one process per GPU. Rank 0
+// calls unique_id() and hands the bytes to the other ranks by the host program's own
+// channel (MPI, a file, a socket). Shared by the partitioned operators built on it.
+class Dist {
+ public:
+  using Id = std::array<uint8_t, TPL_DIST_ID_BYTES>;
+  static Id unique_id() {
+    Id id{};
+    detail::check(tpl_dist_unique_id(id.data()));
+    return id;
+  }
+  Dist(int device, int rank, int nranks, const Id& id) {
+    detail::check(tpl_dist_create(device, rank, nranks, id.data(), &d_));
+  }
+  ~Dist() {
+    if (d_) tpl_dist_destroy(d_);
+  }
+  Dist(const Dist&) = delete;
+  Dist& operator=(const Dist&) = delete;
+  tpl_dist_t handle() const { return d_; }
+
+ private:
+  tpl_dist_t d_ = nullptr;
+};
+
+// How HipCsrOp::partitioned splits a matrix over the ranks (include/tpl.h): replicated
+// long rows (the KKT form), halo-exchange row blocks (any symmetric matrix), or the first
+// that applies.
+enum class Partition { Replicated, Halo, Auto };
+
 // A symmetric sparse matrix resident in HBM (faer LinOp<f64> on SparseColMat<usize, f64>;
 // symmetric, so its CSR arrays are the reference's CSC arrays). Columns ascending per row.
 class HipCsrOp {
@@ -231,12 +262,44 @@ class HipCsrOp {
     detail::check(tpl_op_create_csr(ctx.handle(), n, (int64_t)vals.size(), row_ptr.data(),
                                     col_idx.data(), vals.data(), &op_));
   }
-  ~HipCsrOp() {
-    if (op_) tpl_op_destroy(op_);
+  // This rank's part of the WHOLE matrix (every rank passes the same CSR; collective).
+  // The solvers take it unchanged; b and x are then this rank's rows, local_rows().
+  static HipCsrOp partitioned(std::shared_ptr<Dist> dist, int64_t n,
+                              const std::vector<int64_t>& row_ptr,
+                              const std::vector<int32_t>& col_idx,
+                              const std::vector<double>& vals, Partition how = Partition::Auto) {
+    if (!dist || n < 1 || (int64_t)row_ptr.size() != n + 1 || col_idx.size() != vals.size() ||
+        (int64_t)col_idx.size() != row_ptr.back())
+      throw EngineError(TPL_ERR_INVALID_ARGUMENT, "CSR arrays do not match n / nnz");
+    HipCsrOp op;
+    tpl_status st = TPL_ERR_UNSUPPORTED;
+    if (how != Partition::Halo) {
+      st = tpl_dist_op_create_replicated(dist->handle(), n, row_ptr.data(), col_idx.data(),
+                                         vals.data(), &op.op_);
+      if (st != TPL_OK && (how == Partition::Replicated || st != TPL_ERR_UNSUPPORTED))
+        detail::check(st);
+    }
+    if (st != TPL_OK)
+      detail::check(tpl_dist_op_create_halo(dist->handle(), n, nullptr, row_ptr.data(),
+                                            col_idx.data(), vals.data(), &op.op_));
+    op.dist_ = std::move(dist);
+    return op;
   }
-  HipCsrOp(HipCsrOp&& o) noexcept : op_(std::exchange(o.op_, nullptr)) {}
+  // The global row of each entry of this operator's vectors.
+  std::vector<int64_t> local_rows() const {
+    std::vector<int64_t> rows(std::max<size_t>(nrows(), 1));
+    detail::check(tpl_op_local_rows(op_, rows.data()));
+    rows.resize(nrows());
+    return rows;
+  }
+  ~HipCsrOp() {
+    if (op_) tpl_op_destroy(op_);  // before dist_ (the communicator) is released
+  }
+  HipCsrOp(HipCsrOp&& o) noexcept
+      : op_(std::exchange(o.op_, nullptr)), dist_(std::move(o.dist_)) {}
   HipCsrOp& operator=(HipCsrOp&& o) noexcept {
     std::swap(op_, o.op_);
+    std::swap(dist_, o.dist_);
     return *this;
   }
   HipCsrOp(const HipCsrOp&) = delete;
@@ -253,7 +316,9 @@ class HipCsrOp {
   tpl_op_t handle() const { return op_; }
 
  private:
+  HipCsrOp() = default;
   tpl_op_t op_ = nullptr;
+  std::shared_ptr<Dist> dist_;  // partitioned operators: keeps the communicator alive
 };
 
 namespace detail {

@@ -241,6 +241,37 @@ static void property_tests(const tpl::Context& ctx, const char* dmx, const char*
   CHECK(drift == 0.0, "basis drift %.3e (the engine regenerates V_k bit for bit)", drift);
 }
 
+// ---- the partitioned operator through one RCCL rank (tpl.hpp Dist / HipCsrOp::partitioned):
+// the solvers take it unchanged; its rows cover A once and x agrees with one GPU's
+static void partition_tests(const char* dmx, const char* qfc) {
+  const auto sys = tpl::load_kkt_system(dmx, qfc);
+  const size_t n = (size_t)sys.n, k = 30;
+  auto dist = std::make_shared<tpl::Dist>(0, 0, 1, tpl::Dist::unique_id());
+  tpl::Context ctx(0);
+  tpl::HipCsrOp single(ctx, sys.n, sys.row_ptr, sys.col_idx, sys.vals);
+  const Vec b = std_rng_vector(n);
+  const Vec x1 = tpl::solvers::lanczos_two_pass(single, b, k, tpl::ftk::inv());
+  for (auto how : {tpl::Partition::Auto, tpl::Partition::Halo}) {
+    auto op = tpl::HipCsrOp::partitioned(dist, sys.n, sys.row_ptr, sys.col_idx, sys.vals, how);
+    const auto rows = op.local_rows();
+    CHECK(rows.size() == n, "one rank holds every row (%zu of %zu)", rows.size(), n);
+    std::vector<int> seen(n, 0);
+    for (int64_t r : rows) seen[(size_t)r]++;
+    CHECK(std::all_of(seen.begin(), seen.end(), [](int c) { return c == 1; }), "rows cover A once");
+    Vec bl(rows.size());
+    for (size_t i = 0; i < rows.size(); ++i) bl[i] = b[(size_t)rows[i]];
+    const Vec xl = tpl::solvers::lanczos_two_pass(op, bl, k, tpl::ftk::inv());
+    double d = 0.0, nx = 0.0;
+    for (size_t i = 0; i < rows.size(); ++i) {
+      const double e = xl[i] - x1[(size_t)rows[i]];
+      d += e * e;
+      nx += x1[(size_t)rows[i]] * x1[(size_t)rows[i]];
+    }
+    CHECK(std::sqrt(d) <= 1e-10 * std::sqrt(nx), "partitioned x vs one GPU %.3e",
+          std::sqrt(d / nx));
+  }
+}
+
 // ---- tests/correctness.rs -----------------------------------------------------------------
 static void correctness_tests(const tpl::Context& ctx) {
   const size_t n = 100, k = 30;
@@ -374,6 +405,7 @@ int main(int argc, char** argv) {
       unit_tests(ctx);
       correctness_tests(ctx);
       property_tests(ctx, argv[2], argv[3]);
+      partition_tests(argv[2], argv[3]);
     } catch (const std::exception& e) {
       std::printf("FAIL uncaught: %s\n", e.what());
       ++g_fail;
