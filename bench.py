@@ -12,12 +12,16 @@ resident in HBM before the timed region; x stays in HBM.
 N > 1: when started without torch.distributed.run's environment (no WORLD_SIZE), this
 process launches ``python -m torch.distributed.run --nproc-per-node N ... bench.py`` as
 a CHILD (it never touches the GPU itself) and exits with its status. Each rank drives
-one GPU; together they run ONE row-partitioned solve of BASELINE configs[4] (5M-arc
-synthetic KKT, k = 500; strong scaling), timed between barriers, max over
-ranks; rank 0 then times the same workload on its GPU alone (single_gpu_same_workload).
-At N = 1 the line also carries that workload on one GPU (configs4_5m_1gpu), so a 1 -> N
-curve can be read on one instance. Rehearsal on a one-GPU box: TPL_DEVICE=0
-TPL_DIST_TRANSPORT=host (all ranks share GPU 0, exchanges through host memory).
+one GPU; `value` is ONE row-partitioned solve of the SAME headline workload over the N
+GPUs (replicated long rows, RCCL all-gathers in the pass graphs), timed
+between barriers, max over ranks — strong scaling, so value_N / value_1 is the
+partition's speed-up; rank 0 checks the assembled x against configs2_replicated_N<N> and
+times the same workload on its GPU alone (single_gpu_same_workload). Then BASELINE
+configs[4] (5M arcs) partitioned (`partitioned_configs4`; the N = 1 line carries it on
+one GPU, configs4_5m_1gpu) and the headline on every GPU independently (`replicas`).
+A failed or hung partitioned headline prints `value: null` with its status and exits
+non-zero. Rehearsal on a one-GPU box: TPL_DEVICE=0 TPL_DIST_TRANSPORT=host (all ranks
+share GPU 0, exchanges through host memory).
 
 Extra JSON fields: ``roofline`` for the dominant kernel — SURVEY.md §8(d)'s B_spmv
 = 12 nnz + 4 (n+1) + 16 n per launch over the live HIP-event average launch time of
@@ -72,7 +76,7 @@ def parse(argv=None):
                         "exp: configs[1]'s function)")
     p.add_argument("--arcs", type=int, default=0,
                    help="5000/50000/500000 (netgen fixtures) or any other count (synthetic); "
-                        "default 500000 at N=1, 5000000 (row-partitioned) at N>1")
+                        "default 500000 (the headline; row-partitioned at N > 1)")
     p.add_argument("--partition", type=int, default=-1,
                    help="1: row-partitioned operator even at N=1 (default: N>1)")
     p.add_argument("--single-ref", type=int, default=1,
@@ -104,15 +108,16 @@ def parse(argv=None):
     p.add_argument("--pcie", type=int, default=1, help="N=1: also time host b / x (PCIe)")
     p.add_argument("--parity", type=int, default=1,
                    help="0 to skip the parity block (digests vs tests/golden/parity.json)")
+    p.add_argument("--configs4", type=int, default=1,
+                   help="N > 1: after the partitioned headline, also BASELINE configs[4] (5M "
+                        "arcs) partitioned over the N GPUs (`partitioned_configs4`)")
     p.add_argument("--replicas", type=int, default=1,
-                   help="N > 1: `value` is the headline solve run independently on every GPU "
-                        "(weak scaling, no collective); the row-partitioned configs[4] solve "
-                        "follows in the same run as `partitioned_configs4`. 0: `value` is the "
-                        "partitioned solve itself")
+                   help="N > 1: also the headline solved independently on every GPU (the "
+                        "`replicas` sub-block; never `value`)")
     p.add_argument("--rank-timeout", type=float, default=600.0,
                    help="N > 1: seconds after which every rank gives up (a hung collective); "
-                        "rank 0 then prints the replicas' line with the partitioned phase "
-                        "marked timeout")
+                        "rank 0 then prints a line with no value (the headline hung) or with "
+                        "the phase that hung named")
     p.add_argument("--dist-mode", choices=("auto", "replicated", "rows", "halo"),
                    default="auto",
                    help="partition of the N > 1 solve: replicated long rows (auto: when the "
@@ -148,6 +153,24 @@ def host_info() -> dict:
         pass
     return {"nproc": os.cpu_count(), "allowed_cpus": len(os.sched_getaffinity(0)),
             "cpu_model": model}
+
+
+def cpu_threads_allowed() -> int:
+    """CPU threads this process may really use: the affinity mask, capped by the cgroup's
+    cpu.max quota (a GPU box shows the whole machine's CPUs in the mask but grants one GPU's
+    share) and by OMP_NUM_THREADS when set."""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            quota, period = f.read().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) // int(period))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS", "")
+    if omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    return max(1, n)
 
 
 def load_workload(arcs: int):
@@ -268,6 +291,64 @@ def rocprof_spmv(steps: int, b_spmv: float):
     return out if len(out) > 3 else None
 
 
+def roofline_committed(b_spmv: float, live: dict):
+    """The N = 1 line's `roofline`, every number recomputable from files under profiles/
+    (VERDICT r05 #2): the DOMINANT SpMV kernel by its share of GPU time in the committed
+    rocprofv3 --kernel-trace --stats profile of the headline (profiles/rocprof_headline.json,
+    scripts/update_profiles.py), SURVEY.md §8(d)'s B_spmv over that profile's MEAN launch
+    duration vs 8 TB/s (`frac`; the median beside it), and its PMC bytes per launch from the
+    committed FETCH_SIZE / WRITE_SIZE passes (`traffic`). The same kernel measured live in
+    this run's timed solves rides along as `frac_live` / `avg_launch_us_live` (the rest of
+    the live measurement is the line's `roofline_live`). None when the committed profile
+    measured other kernel sources than this tree's (then the live block stands in)."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "rocprof_headline.json")) as f:
+            rj = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if rj.get("kernel_src_sha16") != kernel_src_digest():
+        return None
+    try:
+        share = {k: float(rj["percentage_of_gpu_time"][k]) for k in ("k_p1_spmv", "k_p2_spmv")}
+        dom = max(share, key=share.get)
+        avg_us = float(rj["avg_ns"][dom]) / 1000.0
+    except (KeyError, TypeError, ValueError):
+        return None
+    gbs = lambda t_us: b_spmv / (t_us * 1e-6) / 1e9
+    pmc_file = "pmc_pass_one.json" if dom == "k_p1_spmv" else "pmc_k_p2_spmv.json"
+    traffic = None
+    try:
+        with open(os.path.join(ROOT, "profiles", pmc_file)) as f:
+            pj = json.load(f)
+        traffic = (pj["traffic_bytes_per_launch"] if dom == "k_p2_spmv" else
+                   next(v["traffic_bytes_per_launch"] for k, v in pj["kernels"].items()
+                        if k.split("::")[-1].startswith(dom + "<")))
+    except (OSError, ValueError, KeyError, StopIteration):
+        pass
+    lk = live.get("kernels", {}).get(dom, {})
+    out = {"bound": "hbm", "kernel": dom, "achieved": round(gbs(avg_us), 1),
+           "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(gbs(avg_us) / HBM_PEAK_GBS, 4),
+           "traffic": traffic,
+           "frac_counter_bytes": None if traffic is None else round(
+               traffic / (avg_us * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+           "bytes_per_launch": b_spmv,
+           "bytes_rule": "SURVEY.md §8(d) B_spmv = 12 nnz + 4 (n+1) + 16 n",
+           "avg_launch_us": round(avg_us, 3),
+           "calls_in_profile": rj.get("calls", {}).get(dom),
+           "share_of_gpu_time_pct": share[dom],
+           "dominant_by": "share of GPU time in the committed rocprofv3 profile",
+           "source": {"avg_launch_us": "profiles/rocprof_headline.json avg_ns (from "
+                                        + str(rj.get("source")) + ")",
+                      "traffic": f"profiles/{pmc_file} (2 x FETCH_SIZE + WRITE_SIZE per launch)"},
+           "profile_kernel_src_sha16": rj.get("kernel_src_sha16"), "matches_build": True,
+           "frac_live": lk.get("frac"), "avg_launch_us_live": lk.get("avg_launch_us_events")}
+    med = (rj.get("median_ns") or {}).get(dom)
+    if med:
+        out["median"] = {"avg_launch_us": round(float(med) / 1000.0, 3),
+                         "frac": round(gbs(float(med) / 1000.0) / HBM_PEAK_GBS, 4)}
+    return out
+
+
 def roofline_block(b_spmv, b_fused, p2_us, p1s_us, p1a_us, n_samp, steps, p1_step_us,
                    solve_s, p2_traffic, p2_traffic_src, p1_traffic, p1_traffic_src, iso,
                    partitioned):
@@ -320,17 +401,25 @@ def roofline_block(b_spmv, b_fused, p2_us, p1s_us, p1a_us, n_samp, steps, p1_ste
     return out
 
 
-RANK_SHARE_FILE = os.path.join(ROOT, "profiles", "rank_share.json")
+RANK_SHARE_FILE = os.path.join(ROOT, "profiles", "rank_share.json")  # configs[4], 5M arcs
+# the headline's shares (configs[2], 500k arcs: scripts/rank_share.py --arcs 500000)
+RANK_SHARE_500K_FILE = os.path.join(ROOT, "profiles", "rank_share_500k.json")
 
 
-def predicted_block(world: int, k: int, steps: int, solve_s: float):
+def rank_share_file(arcs: int) -> str:
+    return RANK_SHARE_500K_FILE if arcs == 500000 else RANK_SHARE_FILE
+
+
+def predicted_block(world: int, k: int, steps: int, solve_s: float, path: str = None):
     """The prediction an N-rank line is held against (scripts/rank_share.py, committed as
-    profiles/rank_share.json): rank 0's share of the replicated partition at this N, solved
-    on one GPU through one RCCL rank — every kernel one rank runs per step, with
-    collectives that move nothing — plus (2 k + k - 1) all-gathers per solve at an unknown
-    latency L each. Beside the measured time: the L it implies."""
+    profiles/rank_share.json for configs[4] and profiles/rank_share_500k.json for the
+    headline): rank 0's share of the replicated partition at this N, solved on one GPU
+    through one RCCL rank — every kernel one rank runs per step, with collectives that move
+    nothing — plus (2 k + k - 1) all-gathers per solve at an unknown latency L each. Beside
+    the measured time: the L it implies."""
+    path = path or RANK_SHARE_FILE
     try:
-        with open(RANK_SHARE_FILE) as f:
+        with open(path) as f:
             rs = json.load(f)
         sh = rs["shares"][str(world)]
     except (OSError, ValueError, KeyError):
@@ -342,12 +431,13 @@ def predicted_block(world: int, k: int, steps: int, solve_s: float):
     # the N-rank solve runs at the pace of its slowest rank's share
     t0 = max(sh.get("ms_per_solve_every_rank") or [one["ms_per_solve"]])
     kern = None
-    try:  # the per-step kernels of the share (rocprofv3 trace medians; N = 8 only)
-        with open(os.path.join(ROOT, "profiles", f"rank_share_n{world}_kernels.json")) as f:
-            kern = json.load(f)
+    try:  # the per-step kernels of the share (rocprofv3 trace medians; 5M, N = 8 only)
+        if path == RANK_SHARE_FILE:
+            with open(os.path.join(ROOT, "profiles", f"rank_share_n{world}_kernels.json")) as f:
+                kern = json.load(f)
     except (OSError, ValueError):
         pass
-    return {"source": f"profiles/rank_share.json ({rs.get('source', 'scripts/rank_share.py')})",
+    return {"source": f"{os.path.relpath(path, ROOT)} ({rs.get('source', 'scripts/rank_share.py')})",
             "rank0_rows": sh["rank0_rows"], "rank0_nnz": sh["rank0_nnz"],
             "ms_every_rank_share": sh.get("ms_per_solve_every_rank"),
             "per_step_us_1rank": {"pass1": one["pass1_us_per_step"],
@@ -365,19 +455,21 @@ def predicted_block(world: int, k: int, steps: int, solve_s: float):
             "implied_L_us": round((1000.0 * solve_s - t0) * 1000.0 / c, 2)}
 
 
-def predicted_curve(k: int, single_ms: float):
+def predicted_curve(k: int, single_ms: float, path: str = None):
     """predicted_block's model for N = 2, 4, 8 at a few all-gather latencies L: ms per
     solve and the speed-up over the one-GPU solve measured in this run."""
+    path = path or RANK_SHARE_FILE
     try:
-        with open(RANK_SHARE_FILE) as f:
+        with open(path) as f:
             rs = json.load(f)
     except (OSError, ValueError):
         return None
     if rs.get("k") != k:
         return None
-    out = {"source": "profiles/rank_share.json (scripts/rank_share.py): rank 0's share of the "
-                     "replicated partition through one RCCL rank + (3k - 1) all-gathers of "
-                     "latency L", "one_gpu_ms": round(single_ms, 3), "N": {}}
+    out = {"source": f"{os.path.relpath(path, ROOT)} (scripts/rank_share.py): the slowest "
+                     "rank's share of the replicated partition through one RCCL rank + "
+                     "(3k - 1) all-gathers of latency L", "one_gpu_ms": round(single_ms, 3),
+           "N": {}}
     for n in ("2", "4", "8"):
         sh = rs.get("shares", {}).get(n)
         if not sh:
@@ -392,12 +484,11 @@ def predicted_curve(k: int, single_ms: float):
 
 
 def run_replicas(args, rank: int, world: int, dist, device: int) -> dict:
-    """N > 1, `value`: the headline workload (BASELINE configs[2]: 500k-arc KKT, two-pass
-    k = 500, f = inv) solved independently on every rank's GPU — one solve's units per GPU,
-    no collective (weak scaling) — K timed solves between barriers, max over ranks. Every
-    rank's x must carry the headline's committed digest (the same bits on every GPU: the
-    order is pinned). Returns the summary rank 0 prints (its own live roofline, and every
-    rank's pass-one step and k_p1_spmv beside it)."""
+    """N > 1, the `replicas` sub-block (context, never `value`): the headline workload
+    (BASELINE configs[2]: 500k-arc KKT, two-pass k = 500, f = inv) solved independently on
+    every rank's GPU — no collective — K timed solves between barriers, max over ranks.
+    Every rank's x must carry the headline's committed digest (the same bits on every GPU:
+    the order is pinned)."""
     import numpy as np
     import torch
 
@@ -418,7 +509,6 @@ def run_replicas(args, rank: int, world: int, dist, device: int) -> dict:
     def solve():
         check(_lib.tpl_lanczos_two_pass(op.handle, bd.data_ptr(), n, args.k, _lib.FTK_INV_PTR,
                                         None, xd.data_ptr(), _lib.TPL_MEM_DEVICE))
-    op.enable_timing(True)
     for _ in range(max(args.warmup, 1)):
         solve()
     torch.cuda.synchronize()
@@ -437,119 +527,288 @@ def run_replicas(args, rank: int, world: int, dist, device: int) -> dict:
     t = torch.tensor([dt], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     dt = float(t.item())
-    p1_us, p2_us, p2_n = op.pass_timing()
-    try:
-        s1_us, a1_us, n_samp = op.step_samples()
-    except Exception:  # noqa: BLE001
-        s1_us = a1_us = None
-        n_samp = 0
     steps = tpl_amd.algorithms.lanczos_pass_one(op, b, args.k).steps_taken
     mine = {"rank": rank, "device": device, "x": x_digest(xd.cpu().numpy()),
-            "ms_per_solve_median": round(1000.0 * sorted(per)[len(per) // 2], 4),
-            "pass1_us_per_step": round(p1_us / steps, 3),
-            "k_p1_spmv_us": None if s1_us is None else round(s1_us, 3),
-            "k_p2_spmv_us": round(p2_us / p2_n, 3)}
+            "ms_per_solve_median": round(1000.0 * sorted(per)[len(per) // 2], 4)}
     every = [None] * world
     dist.all_gather_object(every, mine)
-    b_spmv = op.algo_bytes(_lib.TPL_KERNEL_SPMV)
-    b_fused = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
-    pmc = {}
-    for name in ("pmc_k_p2_spmv.json", "pmc_pass_one.json"):
-        try:
-            with open(os.path.join(ROOT, "profiles", name)) as f:
-                pmc[name] = json.load(f)
-        except (OSError, ValueError):
-            pass
-    p2_tr = pmc.get("pmc_k_p2_spmv.json", {})
-    p1_tr = pmc.get("pmc_pass_one.json", {})
-    p1_traffic = {k.split("::")[-1].split("<")[0]: v["traffic_bytes_per_launch"]
-                  for k, v in p1_tr.get("kernels", {}).items()} or None
-    roof = roofline_block(b_spmv, b_fused, p2_us / p2_n, s1_us, a1_us, n_samp, steps,
-                          p1_us / steps, dt / args.steps, p2_tr.get("traffic_bytes_per_launch"),
-                          p2_tr.get("source"), p1_traffic, p1_tr.get("source"), {}, False)
-    roof["rank"] = 0
     expected = expected_parity().get("headline", {}).get("x")
     op.close()
     del bd, xd
     torch.cuda.empty_cache()
-    iters = world * args.steps * steps
-    return {"value": round(iters / dt, 2), "ms_per_step": round(1000.0 * dt / args.steps, 4),
-            "ms_per_solve_median": mine["ms_per_solve_median"] if rank == 0 else None,
-            "steps_taken": steps, "data": data, "n": n, "nnz": int(a.nnz), "roofline": roof,
+    return {"what": f"the headline solved independently on each of the {world} GPUs (no "
+                    "collective; context for the partitioned `value`, never `value` itself)",
+            "iterations_per_s_all_gpus": round(world * args.steps * steps / dt, 2),
+            "ms_per_step": round(1000.0 * dt / args.steps, 4), "steps_taken": steps,
             "ranks": every,
             "parity": {"ok": expected is not None and all(e["x"] == expected for e in every),
                        "x_expected": expected, "x_every_rank": [e["x"] for e in every]}}
 
 
-def merge_replicas(rep: dict, part: dict, world: int, args) -> dict:
-    """The N > 1 line: `value` from the replicas (weak scaling of the headline), the
-    row-partitioned configs[4] solve of the same run under `partitioned_configs4`."""
-    line = {
-        "metric": METRIC, "value": rep["value"], "unit": "Lanczos iterations/s", "n_gpus": world,
-        "steps": args.steps, "warmup": args.warmup, "ms_per_step": rep["ms_per_step"],
-        "ms_per_solve_median": rep["ms_per_solve_median"], "higher_is_better": True,
-        "scaling": "weak", "vs_baseline": None, "dtype": "f64",
-        "data": rep["data"] + f"; the same solve on each of the {world} GPUs",
-        "config": {"workload": f"lanczos_two_pass k={args.k} f=inv, 500000-arc rho=3 KKT "
-                               f"(n={rep['n']}, nnz={rep['nnz']}), one independent solve per "
-                               f"GPU ({world} replicas, no collective)",
-                   "k": args.k, "steps_taken": rep["steps_taken"],
-                   "order_groups": PINNED_ORDER_GROUPS[500000],
-                   "parallelism": f"replicas{world} (weak scaling: the headline on every GPU)"},
-        "roofline": rep["roofline"], "ranks": rep["ranks"]}
-    parity = {"headline_replicas": rep["parity"]}
-    parity.update(part.get("parity", {}).get("workloads", {}))
-    line["parity"] = {"all_ok": all(v.get("ok") is True for v in parity.values()),
-                      "checked": len(parity), "workloads": parity,
-                      "source": part.get("parity", {}).get("source")}
-    keep = ("value", "unit", "ms_per_step", "ms_per_solve_median", "ms_per_solve_min",
-            "iterations_per_s_median", "config", "roofline", "exchange", "predicted",
-            "single_gpu_same_workload", "data")
-    line["partitioned_configs4"] = dict({k: part[k] for k in keep if k in part},
-                                        scaling="strong")
+def partitioned_solve(args, arcs: int, rank: int, world: int, dist, dctx, device: int) -> dict:
+    """ONE row-partitioned lanczos_two_pass (k = args.k, f = args.f) of the `arcs` workload
+    over the `world` ranks (DistHipCsrOp, --dist-mode; RCCL all-gathers inside the pass
+    graphs): K timed solves between barriers, max over ranks (strong
+    scaling: the total work is the workload's, whatever N). Rank 0 assembles x from every
+    rank's block and checks its digest against tests/golden/parity.json
+    (configs2_<mode>_N<world> for the headline, configs4_<mode>_N<world> for configs[4]),
+    times the same workload on its GPU alone (single_gpu_same_workload) and prints the
+    exchange timing and the rank-share prediction beside it."""
+    import numpy as np
+    import torch
+
+    import tpl_amd
+    from tpl_amd import _lib
+    from tpl_amd.dist import DistHipCsrOp
+    from tpl_amd.error import check
+    tag = f"partitioned {arcs}"
+    stage_marker(f"{tag}: operator")
+    kkt, data = load_workload(arcs)
+    a = kkt.a
+    n = a.shape[0]
+    b = a @ np.full(n, 1.0 / np.sqrt(n))  # src/bin/tradeoff.rs:235-236
+    op = DistHipCsrOp(a, dctx, mode=args.dist_mode)
+    b_loc = op.local(b)
+    b_dev = torch.from_numpy(np.ascontiguousarray(b_loc)).cuda(device)
+    x_dev = torch.empty_like(b_dev)
+    torch.cuda.synchronize()
+    nloc = int(b_dev.shape[0])
+    f_ptr = _lib.FTK_EXP_PTR if args.f == "exp" else _lib.FTK_INV_PTR
+
+    def solve():
+        check(_lib.tpl_lanczos_two_pass(op.handle, b_dev.data_ptr(), nloc, args.k, f_ptr, None,
+                                        x_dev.data_ptr(), _lib.TPL_MEM_DEVICE))
+
+    def barrier():
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+    op.enable_timing(True)
+    stage_marker(f"{tag}: first_solve (graph capture)")
+    for _ in range(max(args.warmup, 0)):
+        solve()
+    stage_marker(f"{tag}: warmup_done")
+    steps_taken = tpl_amd.algorithms.lanczos_pass_one(op, b_loc, args.k).steps_taken
+    barrier()
+    stage_marker(f"{tag}: timed_loop")
+    t0 = time.perf_counter()
+    per_solve = []
+    for _ in range(args.steps):
+        ts = time.perf_counter()
+        solve()
+        per_solve.append(time.perf_counter() - ts)
+    barrier()
+    dt = time.perf_counter() - t0
+    stage_marker(f"{tag}: timed_done")
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    solve_s = dt / args.steps
+    p1_us, p2_us, p2_n = op.pass_timing()
+    b_spmv = op.algo_bytes(_lib.TPL_KERNEL_SPMV)
+    b_fused = op.algo_bytes(_lib.TPL_KERNEL_PASS2_SPMV)
+    x_host = x_dev.cpu().numpy()
+    parts = [None] * world if dist is not None else None
+    mine = (np.asarray(op.local_rows), x_host)
+    if dist is not None:
+        dist.all_gather_object(parts, mine)
+    else:
+        parts = [mine]
+    per_ms = sorted(1000.0 * t for t in per_solve)
+    med_ms = float(np.median(per_ms))
+    mode = op.mode
+    res = {"value": round(args.steps * steps_taken / dt, 2),
+           "unit": "Lanczos iterations/s",
+           "ms_per_step": round(1000.0 * solve_s, 4),
+           "ms_per_solve_median": round(med_ms, 4), "ms_per_solve_min": round(per_ms[0], 4),
+           "iterations_per_s_median": round(steps_taken / (med_ms * 1e-3), 2),
+           "scaling": "strong", "data": data, "mode": mode, "steps_taken": steps_taken,
+           "config": {"workload": f"lanczos_two_pass k={args.k} f={args.f}, {arcs}-arc rho=3 "
+                                  f"KKT (n={n}, nnz={a.nnz}), rows partitioned over {world} GPUs",
+                      "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
+                      "graphs": op.uses_graphs, "rank0_rows": nloc,
+                      "parallelism": f"{mode}{world} (" + {
+                          "replicated": "long-row partials all-gathered per SpMV",
+                          "halo": "halo rows all-gathered per SpMV"}.get(
+                              mode, "vector all-gathered per SpMV") + f", {dctx.transport})"},
+           # rank 0's share, measured live: k_p2_spmv between events around its pass-two
+           # graph (exchanges included); B_spmv of this rank's rows
+           "roofline": roofline_block(b_spmv, b_fused, p2_us / p2_n, None, None, 0, steps_taken,
+                                      p1_us / steps_taken, solve_s, None, None, None, None, {},
+                                      True)}
+    res["roofline"]["rank"] = 0
+    x_full = None
+    if rank == 0:
+        x_full = np.zeros(n)
+        for rows, xs in parts:
+            x_full[rows] = xs
+        res["config"]["x_sha256_16"] = x_digest(x_full)
+        prefix = {500000: "configs2", ARCS_SCALE: "configs4"}.get(arcs)
+        if args.parity and prefix and (args.k, args.f) == (500, "inv"):
+            # halo row blocks reduce in the plain row blocks' order: the same digest
+            key = f"{prefix}_{'rows' if mode == 'halo' else mode}_N{world}"
+            res["parity"] = {key: parity_entry(expected_parity(), key, x=x_digest(x_full))}
+    if args.single_ref:
+        if rank == 0:
+            # the same workload on rank 0's GPU alone (the headline's operator: pinned
+            # order), for the speed-up of the partition and x checked against it
+            op1 = tpl_amd.HipCsrOp(a, device=device)
+            if op1.flags() & 64 and arcs in PINNED_ORDER_GROUPS:
+                op1.set_order_groups(PINNED_ORDER_GROUPS[arcs])
+            bd = torch.from_numpy(b).cuda(device)
+            xd = torch.empty_like(bd)
+
+            def solve1():
+                check(_lib.tpl_lanczos_two_pass(op1.handle, bd.data_ptr(), n, args.k, f_ptr,
+                                                None, xd.data_ptr(), _lib.TPL_MEM_DEVICE))
+            d1 = time_solves(solve1, args.steps, torch.cuda.synchronize)
+            x1 = xd.cpu().numpy()
+            nb = float(np.linalg.norm(b))
+            res["single_gpu_same_workload"] = {
+                "value": round(steps_taken / d1, 2), "ms_per_step": round(1000.0 * d1, 4),
+                "speedup_of_partition": round(d1 / solve_s, 3),
+                # the partition's reduction order differs from one GPU's (rank totals), so
+                # x agrees to rounding before the Krylov process turns chaotic and both
+                # solve A x = b to the same residual after (SURVEY.md §8(c) P3)
+                "x_rel_diff_vs_partitioned": float(np.linalg.norm(x_full - x1)
+                                                   / max(np.linalg.norm(x1), 1e-300)),
+                "residual_partitioned": float(np.linalg.norm(a @ x_full - b) / nb),
+                "residual_single": float(np.linalg.norm(a @ x1 - b) / nb)}
+            op1.close()
+            del bd, xd
+        barrier()
+    # SURVEY.md §8(e) "comm fraction": the exchanges of one pass-one / pass-two step (rank
+    # totals + all-gathers, as the pass graphs issue them) timed alone, every rank together
+    try:  # a diagnostic: its failure must not cost the measured line
+        ex1 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P1, args.profile_iters)
+        ex2 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P2, args.profile_iters)
+        comm_ms = (steps_taken * ex1[0] + (steps_taken - 1) * ex2[0]) / 1000.0
+        res["exchange"] = {"pass1_us_per_step": round(ex1[0], 3),
+                           "pass2_us_per_step": round(ex2[0], 3),
+                           "bytes_received_per_step": [int(ex1[1]), int(ex2[1])],
+                           "ms_per_solve": round(comm_ms, 3),
+                           "comm_frac": round(comm_ms / (1000.0 * solve_s), 4)}
+    except Exception as e:  # noqa: BLE001
+        res["exchange"] = {"error": str(e)}
+    if world > 1 and mode == "replicated" and rank == 0:
+        pred = predicted_block(world, args.k, steps_taken, solve_s, rank_share_file(arcs))
+        if pred is not None:
+            res["predicted"] = pred
+    op.close()
+    del b_dev, x_dev
+    torch.cuda.empty_cache()
+    return res
+
+
+PARITY_SOURCE = ("tests/golden/parity.json: the CPU oracle in the device's reduction order "
+                 "(tests/golden/make_parity.py, pinned by tests/test_parity_digests.py)")
+
+
+def parity_block(workloads: dict) -> dict:
+    return {"all_ok": bool(workloads) and all(v.get("ok") is True for v in workloads.values()),
+            "checked": len(workloads), "source": PARITY_SOURCE, "workloads": workloads}
+
+
+def multi_line(head: dict, world: int, args) -> dict:
+    """The N > 1 line (and bench.py --partition 1 at N = 1): `value` is ONE partitioned solve
+    of the headline (BASELINE configs[2], 500k arcs, k = 500, f = inv) over the N GPUs —
+    strong scaling of the N = 1 line's own workload, so value_N / value_1 is its speed-up."""
+    keep = ("ms_per_step", "ms_per_solve_median", "ms_per_solve_min", "iterations_per_s_median",
+            "data", "config", "roofline", "exchange", "predicted", "single_gpu_same_workload")
+    line = {"metric": METRIC, "value": head["value"], "unit": "Lanczos iterations/s",
+            "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+            "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "status": "ok"}
+    line.update({k: head[k] for k in keep if k in head})
+    line["parity"] = parity_block(dict(head.get("parity", {})))
     return line
 
 
-def partitioned_failure_line(rep: dict, world: int, args, status: str, detail: str) -> dict:
-    """The N > 1 line when the partitioned configs[4] phase failed or hung after the
-    replicas were measured: the replicas' `value` stands, the phase's status beside it."""
-    line = merge_replicas(rep, {}, world, args)
-    line["partitioned_configs4"] = {"status": status, "detail": detail,
-                                    "last_stage_rank0": _PROGRESS["stage"],
-                                    "after_s": round(time.time() - _PROGRESS["t0"], 1)}
-    line["parity"]["all_ok"] = False  # the partitioned digest was never checked
+def sub_phase_failed(line: dict, name: str, status: str, detail: str) -> dict:
+    """A phase after the measured `value` (configs[4] partitioned, replicas) failed or hung:
+    the line keeps its value and names the phase, and its parity verdict is no longer
+    all_ok (the phase's digest was never checked)."""
+    line[name] = {"status": status, "detail": detail, "last_stage_rank0": _PROGRESS["stage"],
+                  "after_s": round(time.time() - _PROGRESS["t0"], 1)}
+    line["status"] = f"{name}: {status}"
+    line["parity"]["all_ok"] = False
     return line
+
+
+def failed_line(world: int, status: str, detail: str) -> dict:
+    """The N > 1 line when the partitioned headline itself failed or hung: no `value`."""
+    return {"metric": METRIC, "value": None, "unit": "Lanczos iterations/s", "n_gpus": world,
+            "higher_is_better": True, "status": status, "detail": detail,
+            "last_stage_rank0": _PROGRESS["stage"],
+            "after_s": round(time.time() - _PROGRESS["t0"], 1)}
 
 
 def rank_watchdog(rank: int, world: int, args):
     """N > 1 under the driver's torchrun (no bench parent to time the ranks out): if the
     run has not finished `args.rank_timeout` s after start — a hung collective — rank 0
-    prints the line it has (the replicas' value, the partitioned phase marked "timeout"
-    with the stage it reached) and every rank exits, instead of the job dying silently."""
+    prints the line it has and every rank exits, instead of the job dying silently. Before
+    the partitioned headline was measured that line has NO value (status "timeout", exit
+    124); after it, the value stands and the phase that hung is named (exit 0)."""
     import threading
 
     def fire():
-        rep = _PROGRESS["replicas"]
+        measured = _PROGRESS["line"]
         if rank == 0:
-            if rep is not None:
-                line = partitioned_failure_line(rep, world, args, "timeout",
-                                                f"not finished after {args.rank_timeout} s")
-            else:
-                line = {"metric": METRIC, "value": None, "unit": "Lanczos iterations/s",
-                        "n_gpus": world, "higher_is_better": True, "status": "timeout",
-                        "last_stage_rank0": _PROGRESS["stage"],
-                        "after_s": round(time.time() - _PROGRESS["t0"], 1)}
-            print(json.dumps(line), flush=True)
-        os._exit(0 if rep is not None else 124)
+            detail = f"not finished after {args.rank_timeout} s"
+            out = (failed_line(world, "timeout", detail) if measured is None else
+                   sub_phase_failed(measured, _PROGRESS["phase"] or "report", "timeout", detail))
+            print(json.dumps(out), flush=True)
+        os._exit(0 if measured is not None else 124)
     t = threading.Timer(args.rank_timeout, fire)
     t.daemon = True
     t.start()
     return t
 
 
+def run_multi(args, rank: int, world: int, dist, device: int) -> None:
+    """N > 1 (and --partition 1): the partitioned headline (the line's `value`), then
+    configs[4] partitioned (`partitioned_configs4`) and the replicas (`replicas`)."""
+    from tpl_amd.dist import DistContext
+    if dist is None:
+        import torch.distributed as dist
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", str(_free_port()))
+        dist.init_process_group("gloo", rank=0, world_size=1)
+    dctx = DistContext(rank, world, device=device,
+                       transport=os.environ.get("TPL_DIST_TRANSPORT", "rccl"))
+    stage_marker("comm_init")
+    arcs = args.arcs or 500000
+    head = partitioned_solve(args, arcs, rank, world, dist, dctx, device)
+    line = multi_line(head, world, args)
+    _PROGRESS["line"] = line
+    if args.configs4 and world > 1 and arcs != ARCS_SCALE:
+        _PROGRESS["phase"] = "partitioned_configs4"
+        try:
+            c4 = partitioned_solve(args, ARCS_SCALE, rank, world, dist, dctx, device)
+            line["partitioned_configs4"] = {k: v for k, v in c4.items() if k != "parity"}
+            line["parity"] = parity_block(dict(line["parity"]["workloads"], **c4.get("parity", {})))
+        except Exception as e:  # noqa: BLE001
+            sub_phase_failed(line, "partitioned_configs4", "failed", f"{type(e).__name__}: {e}")
+    if args.replicas and world > 1:
+        _PROGRESS["phase"] = "replicas"
+        try:
+            rep = run_replicas(args, rank, world, dist, device)
+            line["replicas"] = {k: v for k, v in rep.items() if k != "parity"}
+            wl = dict(line["parity"]["workloads"], headline_replicas=rep["parity"])
+            line["parity"] = parity_block(wl)
+        except Exception as e:  # noqa: BLE001
+            sub_phase_failed(line, "replicas", "failed", f"{type(e).__name__}: {e}")
+    if rank == 0:
+        stage_marker("report")
+        print(json.dumps(line), flush=True)
+    dctx.close()
+
+
 # ---- N > 1: the parent process (never touches the GPU) ------------------------------
-# this rank's progress, for the N > 1 watchdog (rank_watchdog)
-_PROGRESS = {"stage": "start", "t0": time.time(), "replicas": None}
+# this rank's progress, for the N > 1 watchdog (rank_watchdog): the stage it reached, the
+# line once the partitioned headline is measured, and the phase running after it
+_PROGRESS = {"stage": "start", "t0": time.time(), "line": None, "phase": None}
 
 
 def stage_marker(stage: str) -> None:
@@ -683,42 +942,33 @@ def main():
 
     device = int(os.environ.get("TPL_DEVICE", local_rank))  # rehearsal: ranks sharing one GPU
     torch.cuda.set_device(device)
-    rep = run_replicas(args, rank, world, dist, device) if world > 1 and args.replicas else None
-    _PROGRESS["replicas"] = rep
     partitioned = (world > 1) if args.partition < 0 else bool(args.partition)
-    arcs = args.arcs or (ARCS_SCALE if partitioned else 500000)
+    if partitioned:
+        # the row-partitioned headline over the N GPUs
+        run_multi(args, rank, world, dist, device)
+        if dist is not None and world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+    # ---- N = 1: the headline on one GPU, and the other configs beside it
+    arcs = args.arcs or 500000
     kkt, data = load_workload(arcs)
     a = kkt.a
     n = a.shape[0]
     b = a @ np.full(n, 1.0 / np.sqrt(n))  # src/bin/tradeoff.rs:235-236
 
-    dctx = None
     tuned = None
-    if not partitioned:
-        op = tpl_amd.HipCsrOp(a, device=device)
-        b_loc = b
-        groups = (PINNED_ORDER_GROUPS.get(arcs, 0) if args.order_groups < 0
-                  else args.order_groups)
-        if op.flags() & 64:
-            op.set_order_groups(groups)
-        if args.tune_order and op.flags() & 64:
-            # 30 launches per candidate: enough to separate the group counts (0.2-0.8 us
-            # apart), few enough that a rocprofv3 run of this command stays dominated by
-            # the solves' launches
-            tuned = op.tune_order(iters=30)
-    else:
-        # row-partitioned operator: RCCL exchanges over xGMI
-        if dist is None:
-            import torch.distributed as dist
-            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-            os.environ.setdefault("MASTER_PORT", str(_free_port()))
-            dist.init_process_group("gloo", rank=0, world_size=1)
-        from tpl_amd.dist import DistContext, DistHipCsrOp
-        dctx = DistContext(rank, world, device=device,
-                           transport=os.environ.get("TPL_DIST_TRANSPORT", "rccl"))
-        stage_marker("comm_init")
-        op = DistHipCsrOp(a, dctx, mode=args.dist_mode)
-        b_loc = op.local(b)
+    op = tpl_amd.HipCsrOp(a, device=device)
+    b_loc = b
+    groups = (PINNED_ORDER_GROUPS.get(arcs, 0) if args.order_groups < 0
+              else args.order_groups)
+    if op.flags() & 64:
+        op.set_order_groups(groups)
+    if args.tune_order and op.flags() & 64:
+        # 30 launches per candidate: enough to separate the group counts (0.2-0.8 us
+        # apart), few enough that a rocprofv3 run of this command stays dominated by
+        # the solves' launches
+        tuned = op.tune_order(iters=30)
     stage_marker("operator")
     b_dev = torch.from_numpy(np.ascontiguousarray(b_loc)).cuda(device)
     x_dev = torch.empty_like(b_dev)
@@ -742,8 +992,6 @@ def main():
 
     def barrier():
         torch.cuda.synchronize()
-        if dist is not None:
-            dist.barrier()
 
     barrier()
     stage_marker("timed_loop")
@@ -758,10 +1006,6 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     stage_marker("timed_done")
-    if dist is not None:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
 
     # ---- roofline of the dominant kernel, measured live: HIP events recorded inside the
     # last timed solve's pass two (on the operator's stream) bracket its steps_taken - 1
@@ -790,14 +1034,14 @@ def main():
     # FETCH_SIZE and WRITE_SIZE in separate passes, gfx950 correction applied there)
     traffic, traffic_src = None, None
     pmc = os.path.join(ROOT, "profiles", "pmc_k_p2_spmv.json")
-    if os.path.exists(pmc) and arcs == 500000 and not partitioned:
+    if os.path.exists(pmc) and arcs == 500000:
         with open(pmc) as f:
             pj = json.load(f)
         traffic, traffic_src = pj["traffic_bytes_per_launch"], pj["source"]
 
     p1_traffic, p1_traffic_src = None, None
     pmc1 = os.path.join(ROOT, "profiles", "pmc_pass_one.json")
-    if os.path.exists(pmc1) and arcs == 500000 and not partitioned and args.k == 500:
+    if os.path.exists(pmc1) and arcs == 500000 and args.k == 500:
         with open(pmc1) as f:
             pj1 = json.load(f)
         p1_traffic = {k.split("::")[-1].split("<")[0]: v["traffic_bytes_per_launch"]
@@ -810,63 +1054,18 @@ def main():
     # in the device's reduction order (tests/golden/parity.json), outside the timed region
     expected = expected_parity() if args.parity else {}
     parity = {}
-    if args.parity and not partitioned and (arcs, args.k, args.f) == (500000, 500, "inv") \
+    if args.parity and (arcs, args.k, args.f) == (500000, 500, "inv") \
             and op.order_groups() == PINNED_ORDER_GROUPS[500000]:
         parity["headline"] = parity_entry(expected, "headline", x=x_digest(x_host),
                                           coef=x_digest(dec.alphas, dec.betas))
     per_ms = sorted(1000.0 * t for t in per_solve)
     med_ms = per_ms[len(per_ms) // 2] if len(per_ms) % 2 else 0.5 * (per_ms[len(per_ms) // 2 - 1]
                                                                       + per_ms[len(per_ms) // 2])
-    single = None
-    x_full = None
-    if partitioned:
-        # the partitioned x, assembled on rank 0 from every rank's block (gloo, host memory;
-        # replicated long rows carry identical bits on every rank)
-        parts = [None] * world if dist is not None else None
-        mine = (np.asarray(op.local_rows), x_host)
-        if dist is not None:
-            dist.all_gather_object(parts, mine)
-        else:
-            parts = [mine]
-        if rank == 0:
-            x_full = np.zeros(n)
-            for rows, xs in parts:
-                x_full[rows] = xs
-            if args.parity and (arcs, args.k, args.f) == (ARCS_SCALE, 500, "inv"):
-                # halo row blocks reduce in the plain row blocks' order: the same digest
-                key = f"configs4_{'rows' if op.mode == 'halo' else op.mode}_N{world}"
-                parity[key] = parity_entry(expected, key, x=x_digest(x_full))
-    if partitioned and args.single_ref:
-        # the same workload on rank 0's GPU alone, for the speed-up of the partition, and
-        # the partitioned x checked against it
-        if rank == 0:
-            op1 = tpl_amd.HipCsrOp(a, device=device)
-            bd = torch.from_numpy(b).cuda(device)
-            xd = torch.empty_like(bd)
-
-            def solve1():
-                check(_lib.tpl_lanczos_two_pass(op1.handle, bd.data_ptr(), n, args.k,
-                                                _lib.FTK_INV_PTR, None, xd.data_ptr(),
-                                                _lib.TPL_MEM_DEVICE))
-            d1 = time_solves(solve1, args.steps, torch.cuda.synchronize)
-            x1 = xd.cpu().numpy()
-            nb = float(np.linalg.norm(b))
-            single = {"value": round(steps_taken / d1, 2), "ms_per_step": round(1000.0 * d1, 4),
-                      "speedup_of_partition": round(d1 / solve_s, 3),
-                      # the partition's reduction order differs from one GPU's (rank totals),
-                      # so x agrees to rounding before the Krylov process turns chaotic and
-                      # both solve A x = b to the same residual after
-                      "x_rel_diff_vs_partitioned": float(np.linalg.norm(x_full - x1)
-                                                         / max(np.linalg.norm(x1), 1e-300)),
-                      "residual_partitioned": float(np.linalg.norm(a @ x_full - b) / nb),
-                      "residual_single": float(np.linalg.norm(a @ x1 - b) / nb)}
-            op1.close()
-        barrier()
     out = {
         "metric": METRIC,
         "value": round(value, 2),
         "unit": "Lanczos iterations/s",
-        "n_gpus": world,
+        "n_gpus": 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(1000.0 * solve_s, 4),
@@ -875,61 +1074,47 @@ def main():
         "ms_per_solve_min": round(per_ms[0], 4),
         "iterations_per_s_median": round(steps_taken / (med_ms * 1e-3), 2),
         "higher_is_better": True,
-        # N = 1: one headline solve per GPU (the replicas' per-GPU work at N > 1); a
-        # partitioned solve: fixed total work over the ranks
-        "scaling": "strong" if partitioned else "weak",
+        # the same total work at every N: the N > 1 lines partition this solve
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
         "data": data,
         "config": {"workload": f"lanczos_two_pass k={args.k} f={args.f}, {arcs}-arc rho=3 KKT "
-                               f"(n={n}, nnz={a.nnz})"
-                               + ("" if not partitioned else f", rows partitioned over {world} GPUs"),
+                               f"(n={n}, nnz={a.nnz})",
                    "k": args.k, "n": n, "nnz": int(a.nnz), "steps_taken": steps_taken,
                    "graphs": op.uses_graphs,
                    "one_graph_solve": bool(op.flags() & 32),  # f(T_k) on the device
                    # tpl_op_flags bit 6: the device holds the rows in the locality order
                    "row_order": "locality" if op.flags() & 64 else "caller",
-                   **({} if partitioned else {"order_groups": op.order_groups()}),
+                   "order_groups": op.order_groups(),
                    **({} if tuned is None else
                       {"order_tuned": {"groups": tuned[0], "best_us": round(tuned[1], 3)}}),
-                   # bits of the last timed solve's x (rank 0's block): equal across runs
-                   # of one configuration (P0, include/tpl.h tpl_op_set_order_groups)
+                   # bits of the last timed solve's x: equal across runs of one
+                   # configuration (P0, include/tpl.h tpl_op_set_order_groups)
                    "x_sha256_16": x_digest(x_host),
-                   "parallelism": "single" if not partitioned
-                   else (f"{op.mode}{world} (" + {"replicated": "long-row partials all-gathered per SpMV",
-                                                  "halo": "halo rows all-gathered per SpMV"}.get(
-                         op.mode, "vector all-gathered per SpMV")
-                         + f", {dctx.transport})")},
+                   "parallelism": "single"},
         "roofline": roofline_block(b_spmv, b_fused, us, s1_us, a1_us, n_samp, steps_taken,
                                    p1_step_us, solve_s, traffic, traffic_src, p1_traffic,
-                                   p1_traffic_src, iso, partitioned),
+                                   p1_traffic_src, iso, False),
     }
 
-    rp = rocprof_spmv(steps_taken, b_spmv) if (arcs == 500000 and not partitioned) else None
+    if (arcs, args.k) == (500000, 500):
+        # the 1 -> 8 curve of the N > 1 lines (the same solve partitioned), predicted from
+        # the headline's committed rank shares against this run's one-GPU solve
+        curve = predicted_curve(args.k, 1000.0 * solve_s, RANK_SHARE_500K_FILE)
+        if curve is not None:
+            out["predicted_scaling"] = curve
+    rp = rocprof_spmv(steps_taken, b_spmv) if arcs == 500000 else None
     if rp is not None:
         out["roofline"]["committed_profile"] = rp
-    if single is not None:
-        out["single_gpu_same_workload"] = single
-    if partitioned:
-        # SURVEY.md §8(e) "comm fraction": the exchanges of one pass-one / pass-two step
-        # (rank totals + all-gathers, as the pass graphs issue them) timed alone, every
-        # rank together; times the steps of one solve over the solve time (rank 0)
-        try:  # a diagnostic: its failure must not cost the measured line
-            ex1 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P1, args.profile_iters)
-            ex2 = op.profile_kernel(_lib.TPL_KERNEL_EXCHANGE_P2, args.profile_iters)
-            comm_ms = (steps_taken * ex1[0] + (steps_taken - 1) * ex2[0]) / 1000.0
-            out["exchange"] = {"pass1_us_per_step": round(ex1[0], 3),
-                               "pass2_us_per_step": round(ex2[0], 3),
-                               "bytes_received_per_step": [int(ex1[1]), int(ex2[1])],
-                               "ms_per_solve": round(comm_ms, 3),
-                               "comm_frac": round(comm_ms / (1000.0 * solve_s), 4)}
-        except Exception as e:  # noqa: BLE001
-            out["exchange"] = {"error": str(e)}
-    if partitioned and world > 1 and op.mode == "replicated" and rank == 0:
-        pred = predicted_block(world, args.k, steps_taken, solve_s)
-        if pred is not None:
-            out["predicted"] = pred
-    if not partitioned and world == 1 and not args.headline_only:
+    # `roofline` from the committed profiles (recomputable), the live measurement beside it
+    committed = roofline_committed(b_spmv, out["roofline"]) if (arcs, args.k) == (500000, 500) else None
+    if committed is not None:
+        out["roofline_live"] = out["roofline"]
+        out["roofline"] = committed
+    else:
+        out["roofline"]["frac_source"] = "live (no committed profile of this tree's kernels)"
+    if not args.headline_only:
         # the instrumentation's cost: the timed solves ran with live timing on (pass one
         # stamped, the passes in three graphs with events between them); the same solve
         # untimed is ONE graph
@@ -940,7 +1125,7 @@ def main():
                                     "iterations_per_s": round(steps_taken / tu, 2),
                                     "note": "the same solve with live timing off (one device "
                                             "graph, no events or stamps); not `value`"}
-    if args.pcie and not partitioned and world == 1:
+    if args.pcie:
         # PCIe-inclusive rate (never `value`): host b in, host x out, one H2D + one D2H
         xh = np.empty(n)
         bh = np.ascontiguousarray(b)
@@ -953,7 +1138,7 @@ def main():
         out["pcie_inclusive"] = {"iterations_per_s": round(steps_taken / th, 1),
                                  "ms_per_solve": round(1000 * th, 4),
                                  "note": "b and x in host memory (TPL_MEM_HOST)"}
-    if args.one_pass and not partitioned:
+    if args.one_pass:
         # BASELINE configs[3]: lanczos_standard (one pass, V_k in HBM) with CGS2 full
         # re-orthogonalisation, same instance and k; V stays on the device. The sweep
         # rate counts the algorithmic bytes of the re-orthogonalisation (per step j, two
@@ -1019,7 +1204,7 @@ def main():
             "second_passes": second[2], "steps": s1,
             "reorth_GBs": round(rate2, 1), "reorth_frac_of_hbm": round(rate2 / HBM_PEAK_GBS, 4)}
     exp_case = None  # configs[1]: (A, b, device x), checked in the CPU leg
-    if world == 1 and not partitioned and args.other_configs:
+    if args.other_configs:
         # BASELINE configs[0] and [1] on the same GPU (parity-test sizes; reported, not `value`)
         others = {}
         for arcs_o, k_o, f_o, ptr in ((5000, 50, "inv", _lib.FTK_INV_PTR),
@@ -1044,7 +1229,7 @@ def main():
                 exp_case = (ao, bo.cpu().numpy(), xo.cpu().numpy(), k_o)
             opo.close()
         out["other_configs"] = others
-    if world == 1 and not partitioned and args.scale_ref:
+    if args.scale_ref:
         # BASELINE configs[4]'s workload on this one GPU: the N = 1 point of the 1 -> N curve
         # that the N > 1 lines measure (their `value` is this same solve, partitioned)
         k5, _ = load_workload(ARCS_SCALE)
@@ -1081,7 +1266,7 @@ def main():
         curve = predicted_curve(args.k, 1000.0 * d5)
         if curve is not None:
             out["configs4_5m_1gpu"]["predicted_scaling"] = curve
-    if rank == 0 and args.cpu_baseline and world == 1 and not partitioned:
+    if args.cpu_baseline:
         import oracle  # CPU baseline only (reference-order restatement, single thread)
         from oracle import ftk_ref
         o = oracle.Operator(a)
@@ -1113,6 +1298,29 @@ def main():
             "loadavg_before_after": [round(load0[0], 2), round(load1[0], 2)],
             "compiler": ORACLE_CFLAGS, **host_info()}
         out["speedup_vs_cpu"] = round(value / (kc / tc), 1)
+        # beside it, the same restatement on every core this process may use (SURVEY.md
+        # §8(d)): the SpMV and the vector updates split over OpenMP
+        # threads, the dot products and norms serial in the reference's order (bits equal to
+        # the one-thread run's, oracle/lanczos_oracle.c)
+        nthr = cpu_threads_allowed()
+        oracle.set_threads(nthr)
+        load2 = os.getloadavg()
+        times_all = []
+        for _ in range(reps):
+            t1 = time.perf_counter()
+            o.lanczos_two_pass(b, kc, ftk_ref.inv)
+            times_all.append(time.perf_counter() - t1)
+        oracle.set_threads(1)
+        ta = min(times_all)
+        out["cpu_baseline"]["all_cores"] = {
+            "value": round(kc / ta, 2), "unit": "Lanczos iterations/s", "cores": nthr,
+            "sample": f"the same restatement and call on {nthr} OpenMP threads (SpMV and "
+                      f"vector updates parallel, dot products serial), fastest of {reps} calls",
+            "calls_s": [round(t, 3) for t in times_all],
+            "median_value": round(kc / sorted(times_all)[len(times_all) // 2], 2),
+            "loadavg_before": round(load2[0], 2),
+            "threads_rule": "min(sched_getaffinity, cgroup cpu.max quota, OMP_NUM_THREADS)"}
+        out["speedup_vs_cpu_all_cores"] = round(value / (kc / ta), 1)
         if (arcs, args.k, args.f) == (500000, 500, "inv"):
             # context only (not vs_baseline: BASELINE.md publishes times, not this metric):
             # the reference's own CPU times for this solve on its Xeon, one thread
@@ -1134,31 +1342,18 @@ def main():
                                       "ok": rel <= EXP_TOL}
     elif exp_case is not None:
         parity["configs1_exp"] = {"ok": None, "skipped": "needs the CPU leg (--cpu-baseline 1)"}
-    if rank == 0 and parity:
-        out["parity"] = {
-            "all_ok": all(v.get("ok") is True for v in parity.values()),
-            "checked": len(parity),
-            "source": "tests/golden/parity.json: the CPU oracle in the device's reduction "
-                      "order (tests/golden/make_parity.py, pinned by "
-                      "tests/test_parity_digests.py)",
-            "workloads": parity}
-    if rank == 0:
-        if rep is not None:
-            out = merge_replicas(rep, out, world, args)
-        stage_marker("report")
-        print(json.dumps(out), flush=True)
+    if parity:
+        out["parity"] = parity_block(parity)
+    stage_marker("report")
+    print(json.dumps(out), flush=True)
     op.close()
-    if dctx is not None:
-        dctx.close()
-    if dist is not None:
-        dist.barrier()
-        dist.destroy_process_group()
 
 
 def run():
-    """main() with the N > 1 safety net: a rank-local watchdog against hangs, and — when the
-    partitioned phase raises after the replicas were measured — rank 0's line with the
-    replicas' value and the error, instead of no line at all."""
+    """main() with the N > 1 safety net: a rank-local watchdog against hangs, and — when a
+    rank raises — rank 0's line instead of no line at all: with no `value` and a non-zero
+    exit when the partitioned headline itself failed; with the value and the failed phase
+    named when a later phase (configs[4] partitioned, replicas) failed."""
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -1168,13 +1363,14 @@ def run():
     try:
         main()
     except Exception as e:  # noqa: BLE001
-        rep = _PROGRESS["replicas"]
-        if rep is None:
-            raise
+        line = _PROGRESS["line"]
+        detail = f"{type(e).__name__}: {e}"
         if rank == 0:
-            print(json.dumps(partitioned_failure_line(rep, world, args, "failed",
-                                                      f"{type(e).__name__}: {e}")), flush=True)
-        os._exit(0)  # peers blocked in a collective are ended by their own watchdogs
+            out = (failed_line(world, "failed", detail) if line is None else
+                   sub_phase_failed(line, _PROGRESS["phase"] or "report", "failed", detail))
+            print(json.dumps(out), flush=True)
+        # peers blocked in a collective are ended by their own watchdogs
+        os._exit(1 if line is None else 0)
     finally:
         dog.cancel()
 

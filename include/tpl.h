@@ -399,8 +399,34 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
 tpl_status tpl_dist_op_create_halo(tpl_dist_t d, int64_t n, const int64_t* starts,
                                    const int64_t* row_ptr, const int32_t* col_idx,
                                    const double* vals, tpl_op_t* out);
+/* The partition every binding's "auto" takes (Python mode="auto", C++ / Rust
+ * Partition::Auto), decided on the host from the WHOLE matrix for `nranks` ranks, the same
+ * on every rank: TPL_PLAN_REPLICATED when the replicated-long-row split applies (no short
+ * row references another rank's short rows — the KKT case), else TPL_PLAN_HALO when the
+ * halo width H is at most half the widest row block (banded, mesh-like matrices), else
+ * TPL_PLAN_ROWS (the whole vector all-gathered; the three hold the same bits as their
+ * partition oracles, and halo and rows the same bits as each other).                */
+tpl_status tpl_dist_choose_partition(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
+                                     int nranks, int* mode);
+/* This rank's part of the WHOLE matrix in the partition tpl_dist_choose_partition picks
+ * (collective: every rank passes the same CSR); *mode (may be NULL) receives it.    */
+tpl_status tpl_dist_op_create_auto(tpl_dist_t d, int64_t n, const int64_t* row_ptr,
+                                   const int32_t* col_idx, const double* vals, tpl_op_t* out,
+                                   int* mode);
 /* Global row index of each entry of this operator's vectors (tpl_op_nrows entries). */
 tpl_status tpl_op_local_rows(tpl_op_t op, int64_t* rows);
+
+/* Identity key of a caller's compressed-sparse matrix (host only, no device call), for
+ * bindings that accept the caller's own matrix per call and keep its upload (the Rust
+ * shim's `HipOperand for SparseColMatRef`, integration/rust/hip.rs): key[0] hashes the
+ * three arrays' addresses and lengths and n; key[1] an FNV-1a checksum of the first and
+ * last 8 words of each array and `samples` evenly spaced ones. The cost is O(samples),
+ * not O(nnz): a change of addresses, sizes or any sampled word is seen, a change of an
+ * unsampled word is not (callers that mutate a matrix in place re-upload explicitly).
+ * ptr_elem / idx_elem: 4 or 8 (bytes per index).                                      */
+tpl_status tpl_operand_key(int64_t n, const void* ptr_arr, size_t ptr_len, size_t ptr_elem,
+                           const void* idx_arr, size_t idx_len, size_t idx_elem,
+                           const double* vals, size_t nnz, size_t samples, uint64_t* key);
 
 /* ---- host-only plans (no GPU): the reduction order an operator would hold --------
  * The host half of tpl_op_create_csr (mode TPL_PLAN_SINGLE: auto locality order, its

@@ -246,8 +246,10 @@ class Dist {
 };
 
 // How HipCsrOp::partitioned splits a matrix over the ranks (include/tpl.h): replicated
-// long rows (the KKT form), halo-exchange row blocks (any symmetric matrix), or the first
-// that applies.
+// long rows (the KKT form), halo-exchange row blocks (any symmetric matrix), or Auto —
+// tpl_dist_choose_partition's rule, shared with the Python and Rust bindings: replicated
+// when it applies, else halo when the halo is at most half the widest block, else plain
+// row blocks.
 enum class Partition { Replicated, Halo, Auto };
 
 // A symmetric sparse matrix resident in HBM (faer LinOp<f64> on SparseColMat<usize, f64>;
@@ -272,16 +274,15 @@ class HipCsrOp {
         (int64_t)col_idx.size() != row_ptr.back())
       throw EngineError(TPL_ERR_INVALID_ARGUMENT, "CSR arrays do not match n / nnz");
     HipCsrOp op;
-    tpl_status st = TPL_ERR_UNSUPPORTED;
-    if (how != Partition::Halo) {
-      st = tpl_dist_op_create_replicated(dist->handle(), n, row_ptr.data(), col_idx.data(),
-                                         vals.data(), &op.op_);
-      if (st != TPL_OK && (how == Partition::Replicated || st != TPL_ERR_UNSUPPORTED))
-        detail::check(st);
-    }
-    if (st != TPL_OK)
+    if (how == Partition::Replicated)
+      detail::check(tpl_dist_op_create_replicated(dist->handle(), n, row_ptr.data(),
+                                                  col_idx.data(), vals.data(), &op.op_));
+    else if (how == Partition::Halo)
       detail::check(tpl_dist_op_create_halo(dist->handle(), n, nullptr, row_ptr.data(),
                                             col_idx.data(), vals.data(), &op.op_));
+    else
+      detail::check(tpl_dist_op_create_auto(dist->handle(), n, row_ptr.data(), col_idx.data(),
+                                            vals.data(), &op.op_, nullptr));
     op.dist_ = std::move(dist);
     return op;
   }

@@ -25,8 +25,11 @@
 //!   [`HipCsrOp`] (upload once, the fast path), or the very `SparseColMatRef<usize, f64>` /
 //!   `SparseColMat<usize, f64>` the call sites already pass (`&a.as_ref()` in
 //!   src/bin/tradeoff.rs:268-284, src/bin/orthogonality.rs:180-197 and
-//!   tests/correctness.rs:142), uploaded on first use and re-uploaded only when its
-//!   contents change (a content fingerprint, so a mutated matrix never reuses a stale copy).
+//!   tests/correctness.rs:142), uploaded on first use and re-used while its operand key
+//!   (include/tpl.h tpl_operand_key: the arrays' addresses and sizes plus a sampled
+//!   checksum, O(4096) words per call) is unchanged; [`refresh_uploaded`] forces a new
+//!   upload after an in-place change of values. [`HipCsrOp::from_csc`] once and `&op` per
+//!   call is the zero-overhead form.
 //!
 //! `stack` is accepted and left untouched: the engine keeps its workspace in HBM
 //! (faer's `apply_scratch` of [`HipCsrOp`] is empty for the same reason).
@@ -57,7 +60,7 @@ use faer::sparse::{SparseColMat, SparseColMatRef};
 use faer::{Mat, MatMut, MatRef, Par};
 use std::cell::RefCell;
 use std::ffi::{c_char, c_int, c_void, CStr};
-use std::sync::Mutex;
+use std::sync::{Arc, Mutex};
 
 #[repr(C)]
 pub struct TplCtx {
@@ -132,6 +135,12 @@ extern "C" {
     fn tpl_dist_op_create_halo(d: *mut TplDist, n: i64, starts: *const i64,
                                row_ptr: *const i64, col_idx: *const i32, vals: *const f64,
                                out: *mut *mut TplOp) -> c_int;
+    fn tpl_dist_op_create_auto(d: *mut TplDist, n: i64, row_ptr: *const i64,
+                               col_idx: *const i32, vals: *const f64, out: *mut *mut TplOp,
+                               mode: *mut c_int) -> c_int;
+    fn tpl_operand_key(n: i64, ptr_arr: *const c_void, ptr_len: usize, ptr_elem: usize,
+                       idx_arr: *const c_void, idx_len: usize, idx_elem: usize,
+                       vals: *const f64, nnz: usize, samples: usize, key: *mut u64) -> c_int;
 }
 
 fn cstr(p: *const c_char) -> String {
@@ -183,10 +192,12 @@ pub struct HipCsrOp {
     /// this operator's rows: all of A, or this rank's part of a partitioned A
     n: usize,
     /// One engine call at a time per operator (include/tpl.h: not re-entrant); this is
-    /// what makes the operator `Sync`, as faer's `LinOp` requires.
-    lock: Mutex<()>,
+    /// what makes the operator `Sync`, as faer's `LinOp` requires. The operators of one
+    /// communicator share ONE lock (their HipDist's): they share its stream and its RCCL
+    /// communicator, so two of them must never capture graphs or issue collectives at once.
+    lock: Arc<Mutex<()>>,
     /// partitioned: the communicator, kept alive until the operator is destroyed
-    dist: Option<std::sync::Arc<HipDist>>,
+    dist: Option<Arc<HipDist>>,
 }
 
 // SAFETY: the handles are only used under `lock`, and the engine's per-thread error
@@ -217,6 +228,8 @@ fn compact_arrays(a: SparseColMatRef<'_, usize, f64>) -> (Vec<i64>, Vec<i32>, Ve
 }
 
 impl HipCsrOp {
+    /// Upload `a` once (the zero-overhead form: pass `&op` to the solvers below; no
+    /// per-call host work beyond the call itself).
     pub fn from_csc(a: SparseColMatRef<'_, usize, f64>, device: i32)
                     -> Result<Self, LanczosError> {
         if a.nrows() != a.ncols() {
@@ -241,7 +254,7 @@ impl HipCsrOp {
                 return Err(e);
             }
         }
-        Ok(Self { ctx, op, n, lock: Mutex::new(()), dist: None })
+        Ok(Self { ctx, op, n, lock: Arc::new(Mutex::new(())), dist: None })
     }
 
     /// This rank's part of the symmetric `a` over `dist`'s ranks (every rank passes the
@@ -249,9 +262,10 @@ impl HipCsrOp {
     /// `Partition::Replicated` (the KKT form: tpl_dist_op_create_replicated, refused with
     /// a SolverError when a short row references another rank's short rows),
     /// `Partition::Halo` (any symmetric matrix: tpl_dist_op_create_halo over the
-    /// byte-balanced row blocks), `Partition::Auto` (replicated when it applies, else
-    /// halo).
-    pub fn partitioned(a: SparseColMatRef<'_, usize, f64>, dist: &std::sync::Arc<HipDist>,
+    /// byte-balanced row blocks), `Partition::Auto` (tpl_dist_op_create_auto: the rule the
+    /// Python and C++ bindings share — replicated when it applies, else halo when the halo
+    /// is at most half the widest block, else plain row blocks).
+    pub fn partitioned(a: SparseColMatRef<'_, usize, f64>, dist: &Arc<HipDist>,
                        partition: Partition) -> Result<Self, LanczosError> {
         if a.nrows() != a.ncols() {
             return Err(LanczosError(LanczosErrorKind::DimensionMismatch {
@@ -262,23 +276,19 @@ impl HipCsrOp {
         let (rp, ci, v) = compact_arrays(a);
         let n = a.nrows() as i64;
         let mut op = std::ptr::null_mut();
-        const TPL_ERR_UNSUPPORTED: c_int = 104; // the matrix does not allow the split
+        let _g = dist.lock.lock().unwrap();  // the communicator's stream and comm
         unsafe {
-            let mut replicated = false;
-            if partition != Partition::Halo {
-                let st = tpl_dist_op_create_replicated(dist.d, n, rp.as_ptr(), ci.as_ptr(),
-                                                       v.as_ptr(), &mut op);
-                if st != 0 && (partition == Partition::Replicated || st != TPL_ERR_UNSUPPORTED) {
-                    check(st)?;
-                }
-                replicated = st == 0;
-            }
-            if !replicated {
-                check(tpl_dist_op_create_halo(dist.d, n, std::ptr::null(), rp.as_ptr(),
-                                              ci.as_ptr(), v.as_ptr(), &mut op))?;
+            match partition {
+                Partition::Replicated => check(tpl_dist_op_create_replicated(
+                    dist.d, n, rp.as_ptr(), ci.as_ptr(), v.as_ptr(), &mut op))?,
+                Partition::Halo => check(tpl_dist_op_create_halo(
+                    dist.d, n, std::ptr::null(), rp.as_ptr(), ci.as_ptr(), v.as_ptr(), &mut op))?,
+                Partition::Auto => check(tpl_dist_op_create_auto(
+                    dist.d, n, rp.as_ptr(), ci.as_ptr(), v.as_ptr(), &mut op,
+                    std::ptr::null_mut()))?,
             }
             let nl = tpl_op_nrows(op) as usize;
-            Ok(Self { ctx: std::ptr::null_mut(), op, n: nl, lock: Mutex::new(()),
+            Ok(Self { ctx: std::ptr::null_mut(), op, n: nl, lock: dist.lock.clone(),
                       dist: Some(dist.clone()) })
         }
     }
@@ -329,10 +339,14 @@ pub enum Partition {
 /// One rank's RCCL communicator over xGMI (tpl_dist_create).
 pub struct HipDist {
     d: *mut TplDist,
+    /// Held around every engine call that touches this communicator or its stream: every
+    /// operator built on it takes THIS lock as its own (HipCsrOp::lock), so two operators
+    /// sharing an `Arc<HipDist>` never capture graphs or issue collectives concurrently.
+    lock: Arc<Mutex<()>>,
 }
 
-// SAFETY: the communicator is only used by the operators built on it, each under its own
-// lock; the engine serialises the collectives on the operator's stream.
+// SAFETY: the handle is only used under `lock` (operator creation here, every solver call
+// through the operators, which share the lock).
 unsafe impl Send for HipDist {}
 unsafe impl Sync for HipDist {}
 
@@ -349,7 +363,7 @@ impl HipDist {
                -> Result<std::sync::Arc<Self>, LanczosError> {
         let mut d = std::ptr::null_mut();
         unsafe { check(tpl_dist_create(device, rank, nranks, id.as_ptr(), &mut d))? };
-        Ok(std::sync::Arc::new(Self { d }))
+        Ok(Arc::new(Self { d, lock: Arc::new(Mutex::new(())) }))
     }
 }
 
@@ -409,23 +423,42 @@ impl HipOperand for HipCsrOp {
 }
 
 thread_local! {
-    /// The last faer matrix uploaded on this thread: (content fingerprint, operator).
-    static UPLOADED: RefCell<Option<(u64, HipCsrOp)>> = const { RefCell::new(None) };
+    /// The last faer matrix uploaded on this thread: (operand key, operator).
+    static UPLOADED: RefCell<Option<([u64; 2], HipCsrOp)>> = const { RefCell::new(None) };
 }
 
-/// FNV-1a over the words of the compact arrays (dimension, structure and values).
-fn fingerprint(n: usize, rp: &[i64], ci: &[i32], v: &[f64]) -> u64 {
-    let mut h = 0xcbf2_9ce4_8422_2325u64;
-    let mut mix = |w: u64| h = (h ^ w).wrapping_mul(0x0000_0100_0000_01b3);
-    mix(n as u64);
-    rp.iter().for_each(|&p| mix(p as u64));
-    ci.iter().for_each(|&c| mix(c as u64));
-    v.iter().for_each(|&x| mix(x.to_bits()));
-    h
+/// Words of each array the operand key samples (include/tpl.h tpl_operand_key).
+const KEY_SAMPLES: usize = 4096;
+
+/// The identity of `a` as this thread last uploaded it (tpl_operand_key): its three
+/// arrays' addresses and lengths, its dimension, and a checksum of 3 x (KEY_SAMPLES + 16)
+/// words — O(KEY_SAMPLES) host work per solver call (≈10 µs), not the O(nnz) copy and
+/// hash of the whole matrix (that cost sat inside the reference's own timing
+/// window, src/bin/tradeoff.rs:267-286).
+fn operand_key(a: SparseColMatRef<'_, usize, f64>) -> Result<[u64; 2], LanczosError> {
+    let sym = a.symbolic();
+    let (cp, ri, v) = (sym.col_ptr(), sym.row_idx(), a.val());
+    let w = std::mem::size_of::<usize>();
+    let mut key = [0u64; 2];
+    unsafe {
+        check(tpl_operand_key(a.nrows() as i64, cp.as_ptr() as *const c_void, cp.len(), w,
+                              ri.as_ptr() as *const c_void, ri.len(), w, v.as_ptr(), v.len(),
+                              KEY_SAMPLES, key.as_mut_ptr()))?
+    };
+    Ok(key)
+}
+
+/// Forget this thread's upload of a faer matrix: the next solver call uploads it again.
+/// Needed only after changing a matrix's values IN PLACE (same arrays, same sizes) between
+/// calls — the key sees new arrays, new sizes and any change in its sampled words, not a
+/// change of every single word. `HipCsrOp::from_csc` (upload once, pass `&op`) has no
+/// per-call host cost at all and is the form to use in new code.
+pub fn refresh_uploaded() {
+    UPLOADED.with(|cell| *cell.borrow_mut() = None);
 }
 
 /// The reference's call sites pass `&a.as_ref()`: upload on first use (device 0, or
-/// `TPL_DEVICE`), reuse while the contents are unchanged.
+/// `TPL_DEVICE`), reuse while the operand key is unchanged (per call: the key, no copy).
 impl<'a> HipOperand for SparseColMatRef<'a, usize, f64> {
     fn with_hip_op<R, G: FnOnce(&HipCsrOp) -> R>(&self, g: G) -> Result<R, LanczosError> {
         if self.nrows() != self.ncols() {
@@ -434,15 +467,14 @@ impl<'a> HipOperand for SparseColMatRef<'a, usize, f64> {
                 vector_rows: self.nrows(),
             }));
         }
-        let (rp, ci, v) = compact_arrays(*self);
-        let fp = fingerprint(self.nrows(), &rp, &ci, &v);
+        let key = operand_key(*self)?;
         UPLOADED.with(|cell| {
             let mut slot = cell.borrow_mut();
-            if !matches!(&*slot, Some((f, _)) if *f == fp) {
+            if !matches!(&*slot, Some((k, _)) if *k == key) {
                 *slot = None; // free the previous upload before the new one
                 let device = std::env::var("TPL_DEVICE").ok()
                     .and_then(|s| s.parse().ok()).unwrap_or(0);
-                *slot = Some((fp, HipCsrOp::from_arrays(self.nrows(), &rp, &ci, &v, device)?));
+                *slot = Some((key, HipCsrOp::from_csc(*self, device)?));
             }
             Ok(g(&slot.as_ref().unwrap().1))
         })

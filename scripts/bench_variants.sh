@@ -8,7 +8,7 @@ for name in "$@"; do
   python - "$name" <<'PY'
 import json, sys
 d = json.loads(open("/tmp/bv.log").read().strip().splitlines()[-1])
-r = d["roofline"]
+r = d.get("roofline_live", d["roofline"])
 print(json.dumps({"variant": sys.argv[1], "ms": d["ms_per_step"], "p1_step": r["pass1_us_per_step"], "p2_live": r["avg_launch_us_events"], **r["kernels_us_isolated"]}))
 PY
 done

@@ -18,7 +18,7 @@ L = one small all-gather over xGMI at N ranks, the unknown (never measured here:
 per box). bench.py --gpus N (N > 1) prints this next to its measured line and the L
 the measurement implies.
 
-    python scripts/rank_share.py [--k 500] [--ranks 8 4 2 1] [--out FILE]
+    python scripts/rank_share.py [--k 500] [--ranks 8 4 2 1] [--arcs 500000] [--out FILE]
 """
 from __future__ import annotations
 
@@ -44,6 +44,9 @@ def main():
     ap.add_argument("--single", type=int, default=1,
                     help="1: also solve rank 0's share on the single-GPU path (0: the "
                          "one-rank partition only, e.g. under rocprofv3)")
+    ap.add_argument("--arcs", type=int, default=0,
+                    help="workload (bench.load_workload): default BASELINE configs[4] (5M "
+                         "arcs); 500000 for the headline's shares (profiles/rank_share_500k.json)")
     ap.add_argument("--out", default=os.path.join(ROOT, "gpurun_out", "rank_share.json"))
     args = ap.parse_args()
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -56,10 +59,12 @@ def main():
     from tpl_amd.dist import DistContext
     dist.init_process_group("gloo", rank=0, world_size=1)
     torch.cuda.set_device(0)
-    kkt, data = bench.load_workload(bench.ARCS_SCALE)
+    kkt, data = bench.load_workload(args.arcs or bench.ARCS_SCALE)
     a = kkt.a.tocsr()
     ctx = DistContext(0, 1, device=0, transport="rccl")
-    out = {"workload": f"configs[4]: {data}", "k": args.k, "shares": {}}
+    name = "configs[2] (the headline)" if args.arcs == 500000 else "configs[4]"
+    out = {"workload": f"{name}: {data}", "k": args.k, "arcs": args.arcs or bench.ARCS_SCALE,
+           "shares": {}}
     for N in args.ranks:
         res = share(a, N, 0, args, ctx, single=bool(args.single))
         if args.all_ranks and N > 1:

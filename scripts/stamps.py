@@ -21,6 +21,8 @@ sch = op.schedule()
 ns = len(sch["short_rows"])
 CR = int(os.environ.get("CR", "512"))
 nch = (ns + CR - 1) // CR
+# the chunk part of an SpMV grid is padded to 8 ceil(G2 / 8) E / 512 blocks (chunk_of_block)
+NCHB = 8 * ((sch["G2"] + 7) // 8) * (sch["E"] // 512)
 fn = _lib.lib.tpl_debug_stamps
 fn.argtypes = [ctypes.c_void_p, ctypes.c_int]
 def q(x):
@@ -31,7 +33,7 @@ for kid, name in [(3, "spmv"), (2, "p2_spmv"), (0, "p1_spmv")]:
     st = np.zeros(K * 65536, dtype=np.uint64)
     fn(st.ctypes.data, 65536)
     G = int(np.count_nonzero(st[0:K * 60000:K]))  # below kAxpyMarkBase
-    nsl = G - nch
+    nsl = G - NCHB
     m = st[:K * G].reshape(G, K).astype(np.float64)
     m[m == 0] = np.nan
     base = np.nanmin(m[:, 0])
@@ -99,7 +101,7 @@ if os.environ.get("PASS1", "1") == "1":
             ends.append(e)
             hw = st.reshape(65536, K)[:G, 6]
             raw = mm[:G] if rep == 0 else np.concatenate([raw, mm[:G]])
-        nb = G - nch  # bins first in the grid (FIRST=slices)
+        nb = G - NCHB  # bins first in the grid (FIRST=slices)
         os.makedirs(os.path.join(ROOT, "gpurun_out", "diag"), exist_ok=True)
         np.savez(os.path.join(ROOT, "gpurun_out", "diag", "pass1_stamps.npz"), raw=raw.reshape(3, G, K),
                  hw=hw, nbins=nb, nchunks=nch)

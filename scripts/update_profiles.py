@@ -84,7 +84,11 @@ if os.path.exists(mpath):
                 med[k.split("<")[0]] = round(1000.0 * v["median_us"], 1)
 sys.path.insert(0, ROOT)
 from bench import kernel_src_digest  # noqa: E402  (the profile's kernels: this tree's)
-rj = {"config": CFG, "kernel_src_sha16": kernel_src_digest(), "avg_ns": {k: v["avg_ns"] for k, v in stats.items()}, "median_ns": med,
+bline = json.loads(line)
+b_spmv = (bline.get("roofline_live") or bline["roofline"])["bytes_per_launch"]
+rj = {"config": CFG, "kernel_src_sha16": kernel_src_digest(),
+      "bytes_per_launch": b_spmv,  # SURVEY §8(d) B_spmv of the headline (the bench line's)
+      "avg_ns": {k: v["avg_ns"] for k, v in stats.items()}, "median_ns": med,
       "calls": {k: v["calls"] for k, v in stats.items()},
       "percentage_of_gpu_time": {k: v["percentage"] for k, v in stats.items()},
       "source": f"profiles/{tag}_kernel_stats.csv (rocprofv3 --kernel-trace --stats, bench.py "

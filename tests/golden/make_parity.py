@@ -62,6 +62,14 @@ WORKLOADS = {
                                    mode="replicated", nranks=4),
     "configs4_replicated_N8": dict(arcs=5000000, k=500, f="inv", solver="partition",
                                    mode="replicated", nranks=8),
+    # the headline partitioned (bench.py --gpus N, N > 1: the line's `value`, strong
+    # scaling of configs[2]; --dist-mode auto takes the replicated long rows for the KKT)
+    "configs2_replicated_N2": dict(arcs=500000, k=500, f="inv", solver="partition",
+                                   mode="replicated", nranks=2),
+    "configs2_replicated_N4": dict(arcs=500000, k=500, f="inv", solver="partition",
+                                   mode="replicated", nranks=4),
+    "configs2_replicated_N8": dict(arcs=500000, k=500, f="inv", solver="partition",
+                                   mode="replicated", nranks=8),
     # the row-block partition (bench.py --gpus N with TPL_DIST_MODE=rows): every SpMV
     # all-gathers the whole vector
     "configs4_rows_N2": dict(arcs=5000000, k=500, f="inv", solver="partition", mode="rows",
@@ -73,6 +81,10 @@ WORKLOADS = {
 }
 # quick cases the CPU suite recomputes every run (the same code paths at a small k)
 QUICK = {
+    "configs2_replicated_N2_k20": dict(arcs=500000, k=20, f="inv", solver="partition",
+                                       mode="replicated", nranks=2),
+    "configs2_replicated_N8_k20": dict(arcs=500000, k=20, f="inv", solver="partition",
+                                       mode="replicated", nranks=8),
     "configs4_replicated_N2_k20": dict(arcs=5000000, k=20, f="inv", solver="partition",
                                        mode="replicated", nranks=2),
     "configs4_replicated_N8_k20": dict(arcs=5000000, k=20, f="inv", solver="partition",

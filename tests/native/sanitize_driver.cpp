@@ -159,12 +159,20 @@ static void layout_checks() {
   struct Case { int64_t n; int hubs, hub_len; int slices, srm; bool compress; };
   const Case cases[] = {{1, 0, 0, 0, -1, true},      {2, 1, 1, 0, -1, true},     {7, 1, 5, 0, -1, false},
                         {1000, 3, 300, 0, -1, true}, {1000, 3, 300, 8, 2, false}, {20000, 2, 9000, 0, -1, true},
-                        {20000, 40, 700, 2, -1, true}, {5000, 0, 0, 4, 6, true}};
-  for (const Case& c : cases) {
+                        {20000, 40, 700, 2, -1, true}, {5000, 0, 0, 4, 6, true},
+                        // 8 slices and more than 32 bins per slice: crowded CU positions
+                        {20000, 600, 1000, 8, -1, true}};
+  // every bin packing: the first fit, the balanced cut (even and crowd-weighted caps),
+  // the first fit with its lightest bins on the crowded positions
+  const std::pair<int, double> packings[] = {{0, 1.0}, {1, 1.0}, {1, 0.5}, {2, 1.0}};
+  for (const Case& c : cases)
+  for (const auto& pk : packings) {
     std::vector<int32_t> rp, col;
     std::vector<double> val;
     random_csr(c.n, c.hubs, c.hub_len, 1234 + c.n, rp, col, val);
     tpl::SchedParams sp;
+    sp.bin_balance = pk.first;
+    sp.bin_crowd = pk.second;
     sp.slices = c.slices;
     sp.short_row_max = c.srm;
     sp.compress_values = sp.compress_cols = c.compress;

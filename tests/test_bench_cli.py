@@ -161,6 +161,7 @@ def test_prediction_and_roofline_blocks(tmp_path, monkeypatch):
     f.write_text(json.dumps(rs))
     monkeypatch.setattr(bench, "RANK_SHARE_FILE", str(f))
     p = bench.predicted_block(8, 500, 500, 0.030)
+    assert p["source"].startswith(str(f)) or "rank_share.json" in p["source"]
     assert p["ms_at_L_us"]["10"] == round(15.0 + 14.99, 3)
     assert p["implied_L_us"] == round((30.0 - 15.0) * 1000.0 / 1499, 2)
     assert bench.predicted_block(4, 500, 500, 0.03) is None  # no share for N = 4
@@ -184,55 +185,84 @@ def test_prediction_and_roofline_blocks(tmp_path, monkeypatch):
     assert r2["kernel"].startswith("k_p2_spmv") and "all_spmv_time_weighted_frac" not in r2
 
 
-def test_merge_replicas_line():
-    """N > 1: `value` is the replicas' weak-scaled headline throughput; the partitioned
-    configs[4] solve rides along under `partitioned_configs4` (strong scaling), and the
-    parity block covers both."""
+def test_multi_line():
+    """N > 1: `value` is the partitioned headline (strong scaling of the N = 1 workload);
+    configs[4] partitioned and the replicas ride along as sub-blocks, and the parity block
+    covers every workload checked."""
     import argparse
-    rep = {"value": 4 * 57000.0, "ms_per_step": 8.8, "ms_per_solve_median": 8.79,
-           "steps_taken": 500, "data": "netgen 500000-arc", "n": 501155, "nnz": 2000000,
-           "roofline": {"kernel": "k_p1_spmv", "frac": 0.65}, "ranks": [{}] * 4,
-           "parity": {"ok": True, "x_expected": "7bf2409fbbfac620",
-                      "x_every_rank": ["7bf2409fbbfac620"] * 4}}
-    part = {"value": 17000.0, "unit": "Lanczos iterations/s", "ms_per_step": 29.4,
-            "config": {"workload": "5M partitioned"}, "roofline": {"kernel": "k_p2_spmv"},
+    head = {"value": 90000.0, "unit": "Lanczos iterations/s", "ms_per_step": 5.5,
+            "ms_per_solve_median": 5.5, "data": "netgen 500000-arc",
+            "config": {"workload": "500k partitioned"}, "roofline": {"kernel": "k_p2_spmv"},
             "predicted": {"implied_L_us": 10.0}, "exchange": {"comm_frac": 0.5},
-            "parity": {"source": "x", "workloads": {"configs4_replicated_N4": {"ok": True}}}}
+            "parity": {"configs2_replicated_N4": {"ok": True}}}
     args = argparse.Namespace(steps=5, warmup=1, k=500)
-    line = bench.merge_replicas(rep, part, 4, args)
-    assert line["value"] == 228000.0 and line["scaling"] == "weak" and line["n_gpus"] == 4
-    assert line["metric"] == bench.METRIC
-    assert line["partitioned_configs4"]["value"] == 17000.0
-    assert line["partitioned_configs4"]["scaling"] == "strong"
-    assert line["partitioned_configs4"]["predicted"]["implied_L_us"] == 10.0
-    assert line["parity"]["all_ok"] and line["parity"]["checked"] == 2
-    part["parity"]["workloads"]["configs4_replicated_N4"]["ok"] = False
-    assert not bench.merge_replicas(rep, part, 4, args)["parity"]["all_ok"]
+    line = bench.multi_line(head, 4, args)
+    assert line["value"] == 90000.0 and line["scaling"] == "strong" and line["n_gpus"] == 4
+    assert line["metric"] == bench.METRIC and line["status"] == "ok"
+    assert line["predicted"]["implied_L_us"] == 10.0
+    assert line["parity"]["all_ok"] and line["parity"]["checked"] == 1
+    head["parity"]["configs2_replicated_N4"]["ok"] = False
+    assert not bench.multi_line(head, 4, args)["parity"]["all_ok"]
+    # a later phase that failed keeps the value, names the phase, and fails the parity
+    line = bench.sub_phase_failed(bench.multi_line(dict(head, parity={"a": {"ok": True}}), 4,
+                                                   args), "partitioned_configs4", "failed", "x")
+    assert line["value"] == 90000.0 and line["partitioned_configs4"]["status"] == "failed"
+    assert line["status"] == "partitioned_configs4: failed" and not line["parity"]["all_ok"]
+    assert bench.failed_line(4, "failed", "x")["value"] is None
 
 
-def test_rank_watchdog_prints_the_replicas_line(tmp_path):
-    """N > 1 under the driver's torchrun: a rank whose run has not finished by
-    --rank-timeout ends itself; rank 0 first prints the replicas' line with the
-    partitioned phase marked timeout (a hung collective leaves a line, not silence)."""
-    import subprocess
-    code = r"""
+_RANK = r"""
 import json, os, sys, time
 sys.path.insert(0, os.environ["BENCH_ROOT"])
 import bench, argparse
+mode = sys.argv[1]
 args = argparse.Namespace(steps=5, warmup=1, k=500, rank_timeout=1.0)
-bench._PROGRESS["replicas"] = {"value": 2 * 57000.0, "ms_per_step": 8.8, "ms_per_solve_median": 8.8,
-    "steps_taken": 500, "data": "d", "n": 1, "nnz": 1, "roofline": {}, "ranks": [],
-    "parity": {"ok": True}}
-bench.stage_marker("partitioned: first_solve")
-bench.rank_watchdog(0, 2, args)
-time.sleep(30)  # a hung collective
+def fake_main():
+    bench.stage_marker("partitioned 500000: timed_loop")
+    if mode.endswith("late"):  # the headline was measured; a later phase fails / hangs
+        bench._PROGRESS["line"] = bench.multi_line(
+            {"value": 90000.0, "ms_per_step": 5.5, "parity": {"configs2_replicated_N2": {"ok": True}}},
+            2, args)
+        bench._PROGRESS["phase"] = "partitioned_configs4"
+        bench.stage_marker("partitioned 5000000: first_solve (graph capture)")
+    if mode.startswith("hang"):
+        time.sleep(30)  # a hung collective
+    raise RuntimeError("rank 1 lost")
+bench.main = fake_main
+bench.parse = lambda argv=None: args
+bench.run()
 """
+
+
+@pytest.mark.parametrize("mode,rc,value", [("fail", 1, None), ("hang", 124, None),
+                                           ("fail_late", 0, 90000.0),
+                                           ("hang_late", 0, 90000.0)])
+def test_rank_failure_lines(mode, rc, value):
+    """N > 1 under the driver's torchrun (bench.run on rank 0): a partitioned headline that
+    raises or hangs prints a line with NO value and exits non-zero; a
+    later phase that raises or hangs leaves the measured value and names the phase."""
+    import subprocess
     t = time.time()
-    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60,
-                       env=dict(os.environ, BENCH_ROOT=ROOT))
-    assert p.returncode == 0 and time.time() - t < 20
+    p = subprocess.run([sys.executable, "-c", _RANK, mode], capture_output=True, text=True,
+                       timeout=60, env=dict(os.environ, BENCH_ROOT=ROOT, WORLD_SIZE="2", RANK="0"))
+    assert p.returncode == rc, p.stderr[-2000:]
+    assert time.time() - t < 25
     line = json.loads(p.stdout.strip().splitlines()[-1])
-    assert line["value"] == 114000.0 and line["scaling"] == "weak"
-    pc = line["partitioned_configs4"]
-    assert pc["status"] == "timeout" and pc["last_stage_rank0"] == "partitioned: first_solve"
-    assert line["parity"]["all_ok"] is False
+    assert line["value"] == value and line["metric"] == bench.METRIC
+    if value is None:
+        assert line["status"] == ("failed" if mode == "fail" else "timeout")
+        assert line["last_stage_rank0"] == "partitioned 500000: timed_loop"
+    else:
+        pc = line["partitioned_configs4"]
+        assert pc["status"] == ("failed" if mode == "fail_late" else "timeout")
+        assert pc["last_stage_rank0"].startswith("partitioned 5000000")
+        assert line["parity"]["all_ok"] is False and line["scaling"] == "strong"
+
+
+def test_cpu_threads_allowed(monkeypatch):
+    """The all-cores CPU baseline's thread count: the affinity mask, capped by the cgroup
+    quota and OMP_NUM_THREADS (a GPU box's mask shows the whole machine)."""
+    n = bench.cpu_threads_allowed()
+    assert 1 <= n <= len(os.sched_getaffinity(0))
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    assert bench.cpu_threads_allowed() == 1

@@ -394,7 +394,8 @@ def _rust_fns(src):
                   if ":" in p else (p, p)  # a `&self` receiver
                   for p in _split_top(src[i + 1:j - 1])]
         tail = src[j:src.index("{", j)]
-        ret = re.search(r"->\s*(.*?)\s*(?:\bwhere\b|$)", tail, flags=re.S).group(1)
+        rm = re.search(r"->\s*(.*?)\s*(?:\bwhere\b|$)", tail, flags=re.S)
+        ret = rm.group(1) if rm else "()"
         where = tail.split("where", 1)[1] if "where" in tail else ""
         out[m.group(1)] = (gen, params, ret, where)
     return out

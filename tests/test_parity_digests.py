@@ -6,9 +6,10 @@ the CPU oracle in the device's reduction order from the runtime's own host plan
 * the fixture covers every workload the bench times, and its specs are the script's;
 * the host plan is the layout rule conftest restates independently (single GPU, the
   headline's pinned order included), and refuses every device call;
-* the digests recompute: the small and medium workloads and the k = 20 partition cases
-  on every run (about a minute on 8 cores); the k = 500 partitioned and re-orthogonalised
-  ones (minutes each) with TPL_PARITY_FULL=1.
+* the digests recompute: the small and medium workloads, the headline partitioned over 2
+  and 8 ranks (the N > 1 bench lines' `value`, ≈15 s each) and the k = 20 partition cases
+  on every run (about two minutes on 8 cores); the other k = 500 partitioned and
+  re-orthogonalised ones (minutes each) with TPL_PARITY_FULL=1.
 The headline's digest is also the one every round-3 driver bench printed
 (BENCH_r03 config.x_sha256_16 = 7bf2409fbbfac620)."""
 import json
@@ -95,7 +96,8 @@ def _check(name, spec, expected, kkt_tmp):
     assert got == expected, (name, got, expected)
 
 
-@pytest.mark.parametrize("name", ["configs0", "headline", "configs3_one_pass", "configs4_1gpu"])
+@pytest.mark.parametrize("name", ["configs0", "headline", "configs3_one_pass", "configs4_1gpu",
+                                  "configs2_replicated_N2", "configs2_replicated_N8"])
 def test_digests_recompute(fixture, kkt_tmp, name):
     _check(name, make_parity.WORKLOADS[name], fixture["workloads"][name], kkt_tmp)
 
@@ -108,6 +110,7 @@ def test_partition_digests_recompute_k20(fixture, kkt_tmp, name):
 @pytest.mark.skipif(not FULL, reason="minutes per case: TPL_PARITY_FULL=1")
 @pytest.mark.parametrize("name", [n for n in make_parity.WORKLOADS
                                   if n.startswith(("configs3_cgs2", "configs3_selective",
-                                                   "configs4_replicated", "configs4_rows"))])
+                                                   "configs4_replicated", "configs4_rows",
+                                                   "configs2_replicated_N4"))])
 def test_full_digests_recompute(fixture, kkt_tmp, name):
     _check(name, make_parity.WORKLOADS[name], fixture["workloads"][name], kkt_tmp)

@@ -580,65 +580,73 @@ __device__ __forceinline__ void long_bin(const CsrDev& A, int m, int s,
   // add: x + (-0.0) is x bit for bit for every x (signed zeros, infinities and NaNs
   // included), so the sums are unchanged and the select leaves the dependent add chain.
   // Piece sums (canonical long-row order). A piece longer than kBigPiece is summed by a
-  // 16-lane group — lane g sums its entries g + 16q, then the 16-lane butterfly — 16
-  // such pieces per pass (every piece of a bin at once at 500k arcs, where all pieces
-  // are long); those pieces come first in the table (nbig of them).
+  // 16-lane group — lane g sums its entries g + 16q, then the 16-lane butterfly; those
+  // pieces come first in the table (nbig of them). Any other piece is summed by an 8-lane
+  // group — lane g sums its entries g + 8q, then the 8-lane butterfly. The work is dealt
+  // to the 4 waves as wave tasks: big task i sums big pieces 4i .. 4i + 3 (four 16-lane
+  // groups), small task i the other pieces nbig + 8i .. 8i + 7 (eight 8-lane groups); wave
+  // w takes tasks w, w + 4, ... So a bin of, e.g., 9 long and 7 short pieces sums them
+  // in ONE round (3 big tasks + 1 small task) where separate 16-lane and 8-lane rounds
+  // took two — every extra round cost its bin ≈0.4 µs (round-5 stamps, scripts/lab/
+  // bin_cost.py). Which wave sums a piece never enters its sum: the bits are unchanged.
   {
-    const int g16 = t & 15;
-    for (int j0 = 0; j0 < nbig; j0 += kTPB / 16) {
-      const int j = j0 + (t >> 4);
-      const bool valid = j < nbig;
-      const int jc = valid ? j : 0;
-      const int st = starts[jc], nx = starts[jc + 1];
-      const int b0 = valid ? st : 0;
-      const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
-      // this lane's entries k + 16q, q ascending: whole blocks of 8 first (8 reads in
-      // flight, then 8 adds with no bounds test on the chain: the longest pieces run
-      // tens of blocks), then the last 0..7 with the tests
-      int k = b0 + g16;
-      const int cnt = k < en ? (en - k + 15) >> 4 : 0;
-      double acc = 0.0;
-      for (int blk = cnt >> 3; blk > 0; --blk, k += 128) {
-        double v[8];
+    const int lane = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int tb = (nbig + 3) >> 2, ts = (npieces - nbig + 7) >> 3;
+    for (int task = wv; task < tb + ts; task += kTPB / 64) {  // wave-uniform
+      if (task < tb) {
+        const int g16 = lane & 15;
+        const int j = 4 * task + (lane >> 4);
+        const bool valid = j < nbig;
+        const int jc = valid ? j : 0;
+        const int st = starts[jc], nx = starts[jc + 1];
+        const int b0 = valid ? st : 0;
+        const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
+        // this lane's entries k + 16q, q ascending: whole blocks of 8 first (8 reads in
+        // flight, then 8 adds with no bounds test on the chain: the longest pieces run
+        // tens of blocks), then the last 0..7 with the tests
+        int k = b0 + g16;
+        const int cnt = k < en ? (en - k + 15) >> 4 : 0;
+        double acc = 0.0;
+        for (int blk = cnt >> 3; blk > 0; --blk, k += 128) {
+          double v[8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[k + 16 * u];
+          for (int u = 0; u < 8; ++u) v[u] = lds[k + 16 * u];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) acc = acc + v[u];
+          for (int u = 0; u < 8; ++u) acc = acc + v[u];
+        }
+        const int rem = cnt & 7;
+        if (rem > 0) {
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = lds[u < rem ? k + 16 * u : k];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc = acc + (u < rem ? v[u] : -0.0);
+        }
+        acc = group16_sum(acc);
+        if (g16 == 0 && valid) psum[j] = acc;
+      } else {
+        const int g8 = lane & 7;
+        const int j = nbig + 8 * (task - tb) + (lane >> 3);
+        const int jc = j < kTPB - 2 ? j : kTPB - 2;
+        const int st = starts[jc], nx = starts[jc + 1];
+        const bool valid = j < npieces;
+        const int b0 = valid ? st : 0;
+        const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
+        double acc = 0.0;
+        for (int k0 = b0 + g8; k0 < en; k0 += 64) {  // 8 reads in flight, then the adds
+          double v[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) acc = acc + (k0 + 8 * u < en ? v[u] : -0.0);
+        }
+        acc = group8_sum(acc);
+        if (g8 == 0 && valid) psum[j] = acc;
       }
-      const int rem = cnt & 7;
-      if (rem > 0) {
-        double v[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) v[u] = lds[u < rem ? k + 16 * u : k];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) acc = acc + (u < rem ? v[u] : -0.0);
-      }
-      acc = group16_sum(acc);
-      if (g16 == 0 && valid) psum[j] = acc;
     }
   }
   TPL_MARK(7);
-  // The other pieces, 32 per pass: the 8-lane group t >> 3 takes one; its lane g sums
-  // the piece's entries g + 8q, then a butterfly over the 8 lanes.
-  const int g8 = t & 7;
-  for (int j0 = nbig; j0 < npieces; j0 += kTPB / 8) {
-    const int j = j0 + (t >> 3);
-    const int jc = j < kTPB - 2 ? j : kTPB - 2;
-    const int st = starts[jc], nx = starts[jc + 1];
-    const bool valid = j < npieces;
-    const int b0 = valid ? st : 0;
-    const int en = valid ? (nx >= 0 ? nx : -1 - nx) : 0;
-    double acc = 0.0;
-    for (int k0 = b0 + g8; k0 < en; k0 += 64) {  // 8 reads in flight, then the adds
-      double v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = lds[k0 + 8 * u < en ? k0 + 8 * u : k0];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) acc = acc + (k0 + 8 * u < en ? v[u] : -0.0);
-    }
-    acc = group8_sum(acc);
-    if (g8 == 0 && valid) psum[j] = acc;
-  }
   TPL_MARK(8);
   __syncthreads();
   TPL_MARK(3);

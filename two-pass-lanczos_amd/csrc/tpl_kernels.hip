@@ -94,10 +94,15 @@ __device__ __forceinline__ void p1_spmv_body(const CsrDev& A, const DevState& S,
                                              const double* __restrict__ r_cur,
                                              const double* __restrict__ r_prev,
                                              double* __restrict__ W, double* __restrict__ Vcol,
-                                             int j, double* red, double* redb, double* lds) {
+                                             int j, unsigned long long* stamp, double* red,
+                                             double* redb, double* lds) {
+  // every kernel argument in ONE scalar round trip, the launch stamp's pointer included:
+  // a branch on an argument before this point (the stamp test) split the loads into three
+  // dependent round trips ahead of the first vector load (ISA, round 6)
   pin_layout_args(A);
   asm volatile("" ::"s"(S.Pb_r), "s"(S.flags), "s"(S.norms), "s"(S.betas), "s"(S.Pa), "s"(A.G2_r),
-               "s"(xsrc), "s"(r_cur), "s"(r_prev), "s"(W), "s"(Vcol), "s"(j));
+               "s"(xsrc), "s"(r_cur), "s"(r_prev), "s"(W), "s"(Vcol), "s"(j), "s"(stamp));
+  launch_stamp(stamp);
   PartialRegs<NBP> pr;
   load_partials(S.Pb_r, A.G2_r, pr);
   // the stop flag and beta_{j-2} with the partials, ahead of the entries and gathers:
@@ -173,10 +178,9 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 1)) void k_p1_spmv(CsrDev A, 
                                                   double* __restrict__ Vcol, int j,
                                                   unsigned long long* stamp) {
   TPL_MARK_FIRST();
-  launch_stamp(stamp);
   __shared__ double red[4], redb[4];
   extern __shared__ double lds[];
-  p1_spmv_body<F, 1>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
+  p1_spmv_body<F, 1>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp, red, redb, lds);
 }
 // ... and more (four per thread first, the rest in batches; the 5M-arc instance's 1,024
 // row blocks)
@@ -188,10 +192,9 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 4)) void k_p1_spmv_wide(CsrDe
                                                   double* __restrict__ W,
                                                   double* __restrict__ Vcol, int j,
                                                   unsigned long long* stamp) {
-  launch_stamp(stamp);
   __shared__ double red[4], redb[4];
   extern __shared__ double lds[];
-  p1_spmv_body<F, 4>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, red, redb, lds);
+  p1_spmv_body<F, 4>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp, red, redb, lds);
 }
 
 // ---- T_k^{-1} e_1 on the device (the one-graph inv): the host solver's operations
@@ -271,6 +274,12 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
                                                   double* __restrict__ r_next, int j, int k,
                                                   int elim, unsigned long long* stamp) {
   __shared__ double red[4];
+  // every kernel argument in ONE scalar round trip before any branch on one of them (the
+  // stamp and elim tests used to split the loads into three dependent round trips ahead of
+  // the first vector load: ISA, round 6)
+  asm volatile("" ::"s"(A.E), "s"(A.n), "s"(A.norm_n), "s"(A.NA_r), "s"(S.Pa_r), "s"(S.flags),
+               "s"(S.norms), "s"(S.alphas), "s"(S.Pb));
+  asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k), "s"(elim), "s"(stamp));
   launch_stamp(stamp);
   if (elim && blockIdx.x == gridDim.x - 1) {
     if (threadIdx.x != 0 || j < 3) return;
@@ -293,10 +302,6 @@ __global__ __launch_bounds__(kTPB) void k_p1_axpy(CsrDev A, DevState S,
     S.flags[5] = i + 1;
     return;
   }
-  // every kernel argument in one scalar round trip
-  asm volatile("" ::"s"(A.E), "s"(A.n), "s"(A.norm_n), "s"(A.NA_r), "s"(S.Pa_r), "s"(S.flags),
-               "s"(S.norms), "s"(S.alphas), "s"(S.Pb));
-  asm volatile("" ::"s"(W), "s"(r_cur), "s"(r_next), "s"(j), "s"(k));
   const int rb = elem_block(A, blockIdx.x);
   if (rb < 0) return;
   TPL_MARK_AT(kAxpyMarkBase, 0);

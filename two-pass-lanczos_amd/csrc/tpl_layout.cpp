@@ -2,7 +2,6 @@
 #include "tpl_layout.h"
 
 #include <algorithm>
-#include <unordered_set>
 #include <cmath>
 #include <new>
 #include <string>
@@ -175,9 +174,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   L.bin_cap = ((L.bin_cap + kBinMin - 1) / kBinMin) * kBinMin;  // whole load batches
   std::vector<std::vector<std::vector<std::pair<int32_t, int32_t>>>> bins(S); // (r, fill-at-start)
   std::vector<std::vector<int32_t>> fill(S);
-  std::unordered_set<int64_t> lines;  // distinct 128-B lines of the open bin (bin_lines)
   const int segs = sp.bin_segs > 0 && sp.bin_segs < kBinSegs ? sp.bin_segs : kBinSegs;
-  std::vector<int64_t> plines;
   // Only the pieces with entries are packed (a row's empty pieces would only publish
   // +0.0, which its never-written slot already holds; a row with no entries at all keeps
   // its slice-0 piece); pieces_of[r] = the row's packed pieces, its arrival count.
@@ -187,44 +184,165 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
       pieces_of[r] += poff[r * (S + 1) + s + 1] > poff[r * (S + 1) + s];
     pieces_of[r] = std::max(pieces_of[r], 1);
   }
-  int nbig_open = 0, nsmall_open = 0;  // the open bin's long / other pieces
-  for (int s = 0; s < S && nlb > 0; ++s) {
-    lines.clear();
-    for (size_t r = 0; r < nlb; ++r) {
-      const int32_t cnt = poff[r * (S + 1) + s + 1] - poff[r * (S + 1) + s];
-      if (cnt == 0 && !(s == 0 && pieces_of[r] == 1 && poff[r * (S + 1) + S] == poff[r * (S + 1)]))
-        continue;
-      bool over = false;
-      if (sp.bin_lines > 0) {
-        plines.clear();
-        for (int32_t q = poff[r * (S + 1) + s]; q < poff[r * (S + 1) + s + 1]; ++q)
-          if (!lines.count(cmap(col[q]) >> 4)) plines.push_back(cmap(col[q]) >> 4);
-        std::sort(plines.begin(), plines.end());
-        plines.erase(std::unique(plines.begin(), plines.end()), plines.end());
-        over = !lines.empty() && lines.size() + plines.size() > (size_t)sp.bin_lines;
-      }
-      const bool big = cnt > kBigPiece;
-      if (bins[s].empty() || fill[s].back() + cnt > L.bin_cap ||
-          (int)bins[s].back().size() == segs || over ||
-          (big && sp.bin_big > 0 && nbig_open == sp.bin_big) ||
-          (!big && sp.bin_small > 0 && nsmall_open == sp.bin_small)) {
-        bins[s].emplace_back();
-        fill[s].push_back(0);
-        nbig_open = nsmall_open = 0;
-        lines.clear();
-        if (sp.bin_lines > 0) {  // recount the piece against the empty bin
-          plines.clear();
-          for (int32_t q = poff[r * (S + 1) + s]; q < poff[r * (S + 1) + s + 1]; ++q)
-            plines.push_back(cmap(col[q]) >> 4);
+  // Distinct 128-B lines of the gathered vector a bin touches, counted with stamps: line l
+  // belongs to the open bin when bstamp[l] == its epoch, to the piece being weighed when
+  // pstamp[l] == the piece's epoch (epochs only grow, so nothing is ever reset).
+  int64_t max_line = 0;
+  for (size_t r = 0; r < nlb; ++r)
+    for (int32_t q = poff[r * (S + 1)]; q < poff[r * (S + 1) + S]; ++q)
+      max_line = std::max<int64_t>(max_line, cmap(col[q]) >> 4);
+  std::vector<int32_t> bstamp(nlb > 0 ? max_line + 1 : 0, -1), pstamp(bstamp.size(), -1);
+  int32_t bin_epoch = -1, piece_epoch = -1;
+  // Bin packing of slice s: its pieces in row order, cut into contiguous runs (a run of
+  // consecutive rows keeps the locality order's shared lines in one bin). A bin closes
+  // when the next piece would overflow its entries (bin_cap) or pieces (segs), a lab cap,
+  // or — cost >= 0 — the bin's predicted cost. The cost model (fitted to the per-bin
+  // end times of round-5 stamp timelines, scripts/lab/bin_cost.py: end ≈ 3.1 µs + 0.41 µs
+  // per piece-sum round + 1.8 ns per distinct line) in line units: kRoundCost per round
+  // of the wave tasks (long_bin: ceil(big / 4) + ceil(small / 8) tasks, 4 per round) plus
+  // the lines.
+  constexpr int64_t kRoundCost = 228;
+  auto rounds = [](int32_t nbig, int32_t nsmall) {
+    return (int64_t)(((nbig + 3) / 4 + (nsmall + 7) / 8 + 3) / 4);
+  };
+  // Bins that share a CU: with S = 8 the bins of slice s are XCD s's first M workgroups,
+  // and a fully resident grid deals workgroup q of an XCD to CU class q mod 32
+  // (scripts/lab/cu_map.hip, profiles/r02_cu_map.txt) — so when M is not a multiple of 32
+  // the first M mod 32 classes hold one bin more than the others (at 500k: M = 68, classes
+  // 0-3 hold three bins and three chunks, the rest two bins and four chunks). Those
+  // positions m (m mod 32 < M mod 32) are "crowded"; the cut gives them a smaller cost cap
+  // (crowd x the others').
+  constexpr int kCuClasses = 32;  // CUs per XCD (MI355X: 256 CUs / 8 XCDs)
+  auto crowded = [&](int32_t m) {
+    return S == kSlices && L.M > kCuClasses && L.M % kCuClasses != 0 &&
+           m % kCuClasses < L.M % kCuClasses;
+  };
+  auto pack = [&](int s, int64_t cost_cap, double crowd,
+                  std::vector<std::vector<std::pair<int32_t, int32_t>>>& out,
+                  std::vector<int32_t>& fl) {
+    out.clear();
+    fl.clear();
+    int32_t nbig = 0, nsmall = 0;
+    int64_t nlines = 0;
+    // distinct lines of piece rows [q0, q1) not in the open bin (all of them: open = false)
+    auto fresh_lines = [&](int32_t q0, int32_t q1, bool open) {
+      int64_t f = 0;
+      ++piece_epoch;
+      for (int32_t q = q0; q < q1; ++q) {
+        const int64_t l = cmap(col[q]) >> 4;
+        if ((!open || bstamp[l] != bin_epoch) && pstamp[l] != piece_epoch) {
+          pstamp[l] = piece_epoch;
+          ++f;
         }
       }
-      lines.insert(plines.begin(), plines.end());
-      bins[s].back().emplace_back((int32_t)r, fill[s].back());
-      fill[s].back() += cnt;
-      (big ? nbig_open : nsmall_open)++;
+      return f;
+    };
+    for (size_t r = 0; r < nlb; ++r) {
+      const int32_t q0 = poff[r * (S + 1) + s], q1 = poff[r * (S + 1) + s + 1], cnt = q1 - q0;
+      if (cnt == 0 && !(s == 0 && pieces_of[r] == 1 && poff[r * (S + 1) + S] == poff[r * (S + 1)]))
+        continue;
+      const bool big = cnt > kBigPiece;
+      int64_t fresh = fresh_lines(q0, q1, !out.empty());
+      bool close = out.empty();
+      if (!close) {
+        const int32_t nb = nbig + big, ns = nsmall + !big;
+        close = fl.back() + cnt > L.bin_cap || (int)out.back().size() == segs ||
+                (sp.bin_lines > 0 && nlines + fresh > sp.bin_lines) ||
+                (big && sp.bin_big > 0 && nbig == sp.bin_big) ||
+                (!big && sp.bin_small > 0 && nsmall == sp.bin_small) ||
+                (cost_cap >= 0 &&
+                 rounds(nb, ns) * kRoundCost + nlines + fresh >
+                     (crowded((int32_t)out.size() - 1) ? (int64_t)(crowd * (double)cost_cap)
+                                                       : cost_cap));
+        if (close) fresh = fresh_lines(q0, q1, false);  // the piece against an empty bin
+      }
+      if (close) {
+        out.emplace_back();
+        fl.push_back(0);
+        ++bin_epoch;
+        nbig = nsmall = 0;
+        nlines = 0;
+      }
+      for (int32_t q = q0; q < q1; ++q) bstamp[cmap(col[q]) >> 4] = bin_epoch;
+      nlines += fresh;
+      out.back().emplace_back((int32_t)r, fl.back());
+      fl.back() += cnt;
+      (big ? nbig : nsmall)++;
+    }
+  };
+  // predicted cost of bin m of slice s (line units)
+  auto bin_cost = [&](int s, const std::vector<std::pair<int32_t, int32_t>>& bin) {
+    int32_t nb = 0, ns = 0;
+    ++piece_epoch;
+    int64_t nl = 0;
+    for (const auto& p : bin) {
+      const int32_t r = p.first, q0 = poff[r * (S + 1) + s], q1 = poff[r * (S + 1) + s + 1];
+      (q1 - q0 > kBigPiece ? nb : ns)++;
+      for (int32_t q = q0; q < q1; ++q) {
+        const int64_t l = cmap(col[q]) >> 4;
+        if (pstamp[l] != piece_epoch) {
+          pstamp[l] = piece_epoch;
+          ++nl;
+        }
+      }
+    }
+    return bin.empty() ? (int64_t)0 : rounds(nb, ns) * kRoundCost + nl;
+  };
+  // First fit in row order sets M, the bins per slice (the grid never grows). Then
+  // (bin_balance 1) each slice is re-cut into at most M runs whose largest predicted cost
+  // — on crowded positions scaled by 1 / crowd — is the smallest a contiguous cut allows
+  // (the greedy cut under a cost cap uses the fewest bins for that cap, and more cap never
+  // needs more bins: bisect the cap); or (bin_balance 2) the first fit's bins stay and the
+  // lightest of each slice move to its crowded positions. Piece sums are per (row, slice)
+  // and a row's slots are summed in slice order, so which bin holds a piece, and where
+  // that bin runs, never changes a bit.
+  std::vector<std::vector<std::pair<int32_t, int32_t>>> tb;
+  std::vector<int32_t> tf;
+  for (int s = 0; s < S && nlb > 0; ++s) pack(s, -1, 1.0, bins[s], fill[s]);
+  L.M = 0;
+  for (int s = 0; s < S; ++s) L.M = std::max<int32_t>(L.M, (int32_t)bins[s].size());
+  for (int s = 0; s < S && nlb > 0 && sp.bin_balance == 1; ++s) {
+    int64_t lo = 0, hi = 0;  // hi: a cap the first fit's cut meets on every position
+    for (size_t m = 0; m < bins[s].size(); ++m) {
+      const int64_t c = bin_cost(s, bins[s][m]);
+      hi = std::max(hi, crowded((int32_t)m) ? (int64_t)std::ceil((double)c / sp.bin_crowd) + 1 : c);
+    }
+    while (lo < hi) {
+      const int64_t mid = lo + (hi - lo) / 2;
+      pack(s, mid, sp.bin_crowd, tb, tf);
+      if ((int32_t)tb.size() <= L.M) hi = mid;
+      else lo = mid + 1;
+    }
+    pack(s, hi, sp.bin_crowd, bins[s], fill[s]);
+  }
+  if (sp.bin_balance == 2 && nlb > 0 && L.M > kCuClasses && L.M % kCuClasses != 0 && S == kSlices) {
+    for (int s = 0; s < S; ++s) {
+      bins[s].resize(L.M);
+      fill[s].resize(L.M, 0);
+      std::vector<int32_t> ord(L.M);
+      std::vector<int64_t> cost(L.M);
+      for (int32_t m = 0; m < L.M; ++m) {
+        ord[m] = m;
+        cost[m] = bin_cost(s, bins[s][m]);
+      }
+      std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return cost[a] < cost[b]; });
+      int32_t ncrowd = 0;
+      for (int32_t m = 0; m < L.M; ++m) ncrowd += crowded(m);
+      std::vector<int32_t> light(ord.begin(), ord.begin() + ncrowd), rest(ord.begin() + ncrowd, ord.end());
+      std::sort(light.begin(), light.end());
+      std::sort(rest.begin(), rest.end());
+      std::vector<std::vector<std::pair<int32_t, int32_t>>> nb(L.M);
+      std::vector<int32_t> nf(L.M);
+      size_t il = 0, ir = 0;
+      for (int32_t m = 0; m < L.M; ++m) {
+        const int32_t from = crowded(m) ? light[il++] : rest[ir++];
+        nb[m] = std::move(bins[s][from]);
+        nf[m] = fill[s][from];
+      }
+      bins[s] = std::move(nb);
+      fill[s] = std::move(nf);
     }
   }
-  L.M = 0;
   for (int s = 0; s < S; ++s) L.M = std::max<int32_t>(L.M, (int32_t)bins[s].size());
   const size_t nbins = (size_t)S * L.M;
   L.b_col.assign(std::max<size_t>(nbins * L.bin_cap, 1), -1);

@@ -28,6 +28,12 @@ struct SchedParams {
                                     // per bin (their 16-lane sums run kTPB / 16 per pass)
   int bin_small = 0;                // > 0: at most this many other pieces per bin (their
                                     // 8-lane sums run kTPB / 8 per pass)
+  int bin_balance = 1;              // bins per slice after the first fit (tpl_layout.cpp):
+                                    // 0 the first fit, 1 the cost-balanced contiguous cut,
+                                    // 2 the first fit with its lightest bins moved to the
+                                    // crowded CU positions
+  double bin_crowd = 1.0;           // bin_balance 1: cost cap of a crowded position / of
+                                    // the others
 };
 
 // Host copy of the SpMV layout (tpl_device.h).

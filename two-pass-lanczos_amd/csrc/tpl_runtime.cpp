@@ -380,6 +380,8 @@ void rebuild_schedule(tpl_op_s* op) {
   if (const char* e = std::getenv("TPL_BIN_SEGS")) sp.bin_segs = std::atoi(e);
   if (const char* e = std::getenv("TPL_BIN_BIG")) sp.bin_big = std::atoi(e);
   if (const char* e = std::getenv("TPL_BIN_SMALL")) sp.bin_small = std::atoi(e);
+  if (const char* e = std::getenv("TPL_BIN_BALANCE")) sp.bin_balance = std::atoi(e);
+  if (const char* e = std::getenv("TPL_BIN_CROWD")) sp.bin_crowd = std::atof(e);
   if (const char* e = std::getenv("TPL_SLICES")) {  // auto slice count only; the values
     const int s = std::atoi(e);                     // tpl_op_set_slices accepts
     if (sp.slices <= 0 && s > 0 && s <= kSlices && (s & (s - 1)) == 0) sp.slices = s;
@@ -1215,6 +1217,39 @@ void fill_rows(tpl_op_s* op, int R, int me, int64_t n, const int64_t* starts,
     if (q != me)
       for (int64_t c = st[q]; c < st[q + 1]; ++c)
         if (pos[c] >= 0) op->halo_map[c] = (int32_t)(ld + (int64_t)q * H + pos[c]);
+}
+
+// The partition every binding's "auto" takes (tpl_dist_choose_partition): replicated long
+// rows when the matrix allows them, else halo row blocks when the halo is at most half the
+// widest block, else plain row blocks. Host only; the same answer on every rank.
+int choose_partition(int64_t n, const int64_t* row_ptr, const int32_t* col_idx, int R) {
+  if (!row_ptr || R < 1) fail(TPL_ERR_INVALID_ARGUMENT, "bad argument");
+  {
+    tpl_op_s tmp;
+    tpl_dist_s pd;
+    pd.nranks = R;
+    tmp.dist = &pd;
+    // the split's feasibility does not depend on the rank; the values are not read for it
+    std::vector<double> ones(std::max<int64_t>(row_ptr[n], 1), 1.0);
+    try {
+      fill_replicated(&tmp, R, 0, n, row_ptr, col_idx, ones.data());
+      tmp.dist = nullptr;
+      return TPL_PLAN_REPLICATED;
+    } catch (const Error& e) {
+      tmp.dist = nullptr;
+      if (e.code != TPL_ERR_UNSUPPORTED) throw;
+    }
+  }
+  tpl_op_s tmp;
+  tpl_dist_s pd;
+  pd.nranks = R;
+  tmp.dist = &pd;
+  std::vector<double> ones(std::max<int64_t>(row_ptr[n], 1), 1.0);
+  fill_rows(&tmp, R, 0, n, nullptr, row_ptr, col_idx, ones.data(), true);
+  tmp.dist = nullptr;
+  int64_t widest = 0;
+  for (int r = 0; r < R; ++r) widest = std::max<int64_t>(widest, tmp.starts[r + 1] - tmp.starts[r]);
+  return 2 * tmp.hH <= widest ? TPL_PLAN_HALO : TPL_PLAN_ROWS;
 }
 
 } // namespace
@@ -2149,6 +2184,74 @@ tpl_status tpl_dist_op_create_replicated(tpl_dist_t d, int64_t n, const int64_t*
     fill_replicated(op.get(), d->nranks, d->rank, n, row_ptr, col_idx, vals);
     init_op(op.get());
     *out = op.release();
+  });
+}
+
+tpl_status tpl_dist_choose_partition(int64_t n, const int64_t* row_ptr, const int32_t* col_idx,
+                                     int nranks, int* mode) {
+  return guarded([&] {
+    if (!mode) fail(TPL_ERR_INVALID_ARGUMENT, "mode is NULL");
+    *mode = choose_partition(n, row_ptr, col_idx, nranks);
+  });
+}
+
+tpl_status tpl_dist_op_create_auto(tpl_dist_t d, int64_t n, const int64_t* row_ptr,
+                                   const int32_t* col_idx, const double* vals, tpl_op_t* out,
+                                   int* mode) {
+  return guarded([&] {
+    if (!d || !row_ptr || !out) fail(TPL_ERR_INVALID_ARGUMENT, "NULL argument");
+    const int m = choose_partition(n, row_ptr, col_idx, d->nranks);
+    HIPCHK(hipSetDevice(d->ctx.device));
+    auto op = std::make_unique<tpl_op_s>();
+    op->ctx = &d->ctx;
+    op->device = d->ctx.device;
+    op->stream = d->ctx.stream;
+    op->dist = d;
+    op->eager = d->comm == nullptr;
+    if (m == TPL_PLAN_REPLICATED)
+      fill_replicated(op.get(), d->nranks, d->rank, n, row_ptr, col_idx, vals);
+    else
+      fill_rows(op.get(), d->nranks, d->rank, n, nullptr, row_ptr, col_idx, vals,
+                m == TPL_PLAN_HALO);
+    init_op(op.get());
+    if (mode) *mode = m;
+    *out = op.release();
+  });
+}
+
+tpl_status tpl_operand_key(int64_t n, const void* ptr_arr, size_t ptr_len, size_t ptr_elem,
+                           const void* idx_arr, size_t idx_len, size_t idx_elem,
+                           const double* vals, size_t nnz, size_t samples, uint64_t* key) {
+  return guarded([&] {
+    if (!key) fail(TPL_ERR_INVALID_ARGUMENT, "key is NULL");
+    if ((ptr_len && !ptr_arr) || (idx_len && !idx_arr) || (nnz && !vals))
+      fail(TPL_ERR_INVALID_ARGUMENT, "NULL array with a nonzero length");
+    if ((ptr_elem != 4 && ptr_elem != 8) || (idx_elem != 4 && idx_elem != 8))
+      fail(TPL_ERR_INVALID_ARGUMENT, "index element size must be 4 or 8 bytes");
+    uint64_t h = 0xcbf29ce484222325ull;  // FNV-1a over 64-bit words
+    auto mix = [&](uint64_t w) { h = (h ^ w) * 0x100000001b3ull; };
+    // identity: the arrays' addresses and lengths, the dimension
+    for (uint64_t w : {(uint64_t)n, (uint64_t)(uintptr_t)ptr_arr, (uint64_t)ptr_len,
+                       (uint64_t)(uintptr_t)idx_arr, (uint64_t)idx_len,
+                       (uint64_t)(uintptr_t)vals, (uint64_t)nnz})
+      mix(w);
+    key[0] = h;
+    // contents: the first and last 8 words of each array and `samples` evenly spaced
+    // ones (positions i * len / samples), so the check costs O(samples), not O(nnz)
+    h = 0xcbf29ce484222325ull;
+    auto sample = [&](const void* a, size_t len, size_t elem) {
+      auto word = [&](size_t i) {
+        return elem == 8 ? ((const uint64_t*)a)[i] : (uint64_t)((const uint32_t*)a)[i];
+      };
+      for (size_t i = 0; i < std::min<size_t>(len, 8); ++i) mix(word(i));
+      for (size_t i = len > 8 ? len - 8 : len; i < len; ++i) mix(word(i));
+      if (len > 16)
+        for (size_t s = 0; s < samples; ++s) mix(word((size_t)((unsigned __int128)s * len / samples)));
+    };
+    sample(ptr_arr, ptr_len, ptr_elem);
+    sample(idx_arr, idx_len, idx_elem);
+    sample(vals, nnz, 8);
+    key[1] = h;
   });
 }
 

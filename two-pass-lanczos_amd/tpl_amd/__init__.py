@@ -12,7 +12,7 @@ src/lib.rs:94-101) on top of the C ABI of libtpl_amd.so (include/tpl.h):
 from . import _lib
 from . import algorithms, error, ftk, solvers
 from .error import DataLoaderError, LanczosError, LanczosErrorKind, TplError
-from .operator import HipCsrOp, HostPlan, device_count, locality_order
+from .operator import HipCsrOp, HostPlan, device_count, locality_order, refresh_uploaded
 from .solvers import lanczos, lanczos_two_pass
 
 __version__ = "0.1.0"
@@ -21,5 +21,5 @@ LIB_PATH = _lib.LIB_PATH
 __all__ = [
     "lanczos", "lanczos_two_pass", "algorithms", "solvers", "error", "ftk", "HipCsrOp",
     "LanczosError", "LanczosErrorKind", "TplError", "DataLoaderError", "device_count",
-    "locality_order", "HostPlan",
+    "locality_order", "HostPlan", "refresh_uploaded",
 ]

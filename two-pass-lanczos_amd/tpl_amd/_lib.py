@@ -206,6 +206,13 @@ tpl_dist_op_create_replicated = _sig("tpl_dist_op_create_replicated", c_int, c_v
 tpl_dist_op_create_halo = _sig("tpl_dist_op_create_halo", c_int, c_void_p, c_int64, POINTER(c_int64),
                                POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p))
 tpl_op_local_rows = _sig("tpl_op_local_rows", c_int, c_void_p, POINTER(c_int64))
+tpl_dist_choose_partition = _sig("tpl_dist_choose_partition", c_int, c_int64, POINTER(c_int64),
+                                 POINTER(c_int32), c_int, POINTER(c_int))
+tpl_dist_op_create_auto = _sig("tpl_dist_op_create_auto", c_int, c_void_p, c_int64,
+                               POINTER(c_int64), POINTER(c_int32), PD, POINTER(c_void_p),
+                               POINTER(c_int))
+tpl_operand_key = _sig("tpl_operand_key", c_int, c_int64, c_void_p, c_size_t, c_size_t, c_void_p,
+                       c_size_t, c_size_t, PD, c_size_t, c_size_t, POINTER(ctypes.c_uint64))
 # host-only plans (include/tpl.h "host-only plans")
 TPL_PLAN_SINGLE, TPL_PLAN_REPLICATED, TPL_PLAN_ROWS, TPL_PLAN_HALO = 0, 1, 2, 3
 tpl_plan_create = _sig("tpl_plan_create", c_int, c_int64, POINTER(c_int64), POINTER(c_int32), PD,
@@ -213,4 +220,5 @@ tpl_plan_create = _sig("tpl_plan_create", c_int, c_int64, POINTER(c_int64), POIN
 EXPORTED += ["tpl_plan_create"]
 EXPORTED += ["tpl_dist_op_create_replicated", "tpl_op_local_rows", "tpl_dist_partition", "tpl_dist_unique_id", "tpl_dist_create",
              "tpl_dist_create_host", "tpl_dist_destroy", "tpl_dist_op_create_csr",
-             "tpl_dist_op_create_halo"]
+             "tpl_dist_op_create_halo", "tpl_dist_choose_partition", "tpl_dist_op_create_auto",
+             "tpl_operand_key"]

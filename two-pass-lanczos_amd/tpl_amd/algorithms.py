@@ -29,7 +29,7 @@ import numpy as np
 from . import _lib
 from ._vec import Vec
 from .error import check
-from .operator import HipCsrOp
+from .operator import HipCsrOp, as_operator
 
 BREAKDOWN_TOLERANCE = 1000.0 * np.finfo(np.float64).eps  # src/algorithms/mod.rs:140-143
 
@@ -78,9 +78,8 @@ class DeviceBasisView:
 
 
 def _op(operator) -> HipCsrOp:
-    if not isinstance(operator, HipCsrOp):
-        raise TypeError("operator must be a tpl_amd.HipCsrOp (device-resident CSR operator)")
-    return operator
+    """A HipCsrOp, or the caller's scipy matrix uploaded once (operator.as_operator)."""
+    return as_operator(operator)
 
 
 def _reorth_mode(r) -> int:

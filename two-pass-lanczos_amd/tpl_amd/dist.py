@@ -39,6 +39,21 @@ def halo_width(a, starts) -> int:
                            minlength=len(starts) - 1).max())
 
 
+_MODE_NAMES = {_lib.TPL_PLAN_REPLICATED: "replicated", _lib.TPL_PLAN_ROWS: "rows",
+               _lib.TPL_PLAN_HALO: "halo"}
+
+
+def choose_partition(a, nranks: int) -> str:
+    """The partition mode="auto" takes for `nranks` ranks (tpl_dist_choose_partition, the
+    rule every binding shares; host only): "replicated", "halo" or "rows"."""
+    n, rp, ci, _ = _as_csr_arrays(a)
+    m = ctypes.c_int()
+    check(_lib.tpl_dist_choose_partition(n, rp.ctypes.data_as(POINTER(c_int64)),
+                                         ci.ctypes.data_as(POINTER(c_int32)), int(nranks),
+                                         byref(m)))
+    return _MODE_NAMES[m.value]
+
+
 def partition(a, nranks: int) -> np.ndarray:
     """starts[nranks + 1] of the byte-balanced contiguous row blocks (tpl_dist_partition)."""
     n, rp, _, _ = _as_csr_arrays(a)
@@ -109,9 +124,10 @@ class DistHipCsrOp(HipCsrOp):
     mode "rows" (tpl_dist_op_create_csr): contiguous row blocks, the whole vector
     all-gathered per SpMV; mode "halo" (tpl_dist_op_create_halo): the same blocks and
     bits, only the rows another rank references all-gathered (``halo_width`` per rank);
-    "auto": replicated when the matrix allows it (no short row references another
-    rank's short rows — the KKT case), else halo when its width is at most half the
-    widest block (a banded or mesh-like matrix), else rows.
+    "auto" (tpl_dist_op_create_auto, the rule the C++ and Rust bindings share):
+    replicated when the matrix allows it (no short row references another rank's short
+    rows — the KKT case), else halo when its width is at most half the widest block (a
+    banded or mesh-like matrix), else rows.
     ``local_rows``: global row of each entry of this rank's vectors (``local(v)``).
     """
 
@@ -122,19 +138,30 @@ class DistHipCsrOp(HipCsrOp):
         self.n_global = n
         h = c_void_p()
         self.mode = None
-        if mode in ("auto", "replicated") and starts is None:
+        if mode == "auto" and starts is None:
+            m = ctypes.c_int()
+            check(_lib.tpl_dist_op_create_auto(
+                ctx.handle, n, rp.ctypes.data_as(POINTER(c_int64)),
+                ci.ctypes.data_as(POINTER(c_int32)), v.ctypes.data_as(POINTER(c_double)),
+                byref(h), byref(m)))
+            self.mode = _MODE_NAMES[m.value]
+            if self.mode != "replicated":
+                self.starts = partition((n, rp, ci, v), ctx.world)
+        if mode == "replicated" and starts is None:
             st = _lib.tpl_dist_op_create_replicated(
                 ctx.handle, n, rp.ctypes.data_as(POINTER(c_int64)),
                 ci.ctypes.data_as(POINTER(c_int32)), v.ctypes.data_as(POINTER(c_double)),
                 byref(h))
             if st == _lib.TPL_OK:
                 self.mode = "replicated"
-            elif mode == "replicated" or st != _lib.TPL_ERR_UNSUPPORTED:
+            else:
                 check(st)
         if self.mode is None:
             self.starts = (partition((n, rp, ci, v), ctx.world) if starts is None
                            else np.ascontiguousarray(starts, dtype=np.int64))
         if self.mode is None and mode in ("auto", "halo"):
+            # explicit starts: halo when asked, or (auto) when it is at most half the widest
+            # block — tpl_dist_choose_partition's rule over the caller's split
             if mode == "halo" or 2 * halo_width((n, rp, ci, v), self.starts) <= int(
                     np.diff(self.starts).max()):
                 check(_lib.tpl_dist_op_create_halo(
@@ -143,7 +170,7 @@ class DistHipCsrOp(HipCsrOp):
                     v.ctypes.data_as(POINTER(c_double)), byref(h)))
                 self.mode = "halo"
         if self.mode is None:
-            if mode not in ("auto", "rows", "replicated"):
+            if mode not in ("auto", "rows"):
                 raise ValueError(f"unknown partition mode {mode!r}")
             r0, r1 = int(self.starts[ctx.rank]), int(self.starts[ctx.rank + 1])
             lrp = np.ascontiguousarray(rp[r0:r1 + 1] - rp[r0], dtype=np.int64)

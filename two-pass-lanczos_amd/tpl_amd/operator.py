@@ -318,3 +318,54 @@ class HipCsrOp:
 
 
 HostPlan.schedule = HipCsrOp.schedule
+
+
+# -- the caller's own matrix as `operator` (the reference's call sites pass `&a.as_ref()`,
+# src/bin/tradeoff.rs:268-284): upload on first use, re-use while its operand key is unchanged
+KEY_SAMPLES = 4096  # words of each array the key's checksum samples (tpl_operand_key)
+_uploaded = threading.local()
+
+
+def operand_key(a) -> tuple:
+    """include/tpl.h tpl_operand_key of a scipy CSR / CSC matrix's OWN arrays (no copy):
+    (identity: the arrays' addresses and sizes and n, checksum of the first and last 8 and
+    KEY_SAMPLES evenly spaced words of each) — O(KEY_SAMPLES) host work, not O(nnz)."""
+    ip, ix, v = a.indptr, a.indices, a.data
+    for arr in (ip, ix):
+        if arr.dtype.itemsize not in (4, 8) or not arr.flags.c_contiguous:
+            raise TypeError("index arrays must be contiguous 32- or 64-bit integers")
+    if v.dtype != np.float64 or not v.flags.c_contiguous:
+        raise TypeError("values must be a contiguous float64 array")
+    key = (ctypes.c_uint64 * 2)()
+    check(_lib.tpl_operand_key(int(a.shape[0]), ip.ctypes.data, ip.size, ip.dtype.itemsize,
+                               ix.ctypes.data, ix.size, ix.dtype.itemsize,
+                               v.ctypes.data_as(POINTER(c_double)), v.size, KEY_SAMPLES, key))
+    return (int(key[0]), int(key[1]))
+
+
+def _upload(a, device: int) -> "HipCsrOp":
+    return HipCsrOp(a, device=device)
+
+
+def as_operator(operator, device: int = 0) -> "HipCsrOp":
+    """A solver's `operator`: a HipCsrOp as is (the zero-overhead form), or a scipy sparse
+    matrix uploaded on first use and re-used on this thread while its operand key is
+    unchanged (the Rust shim's `HipOperand for SparseColMatRef` rule,
+    integration/rust/hip.rs). After changing a matrix's values IN PLACE call
+    ``refresh_uploaded()``: the key sees new arrays, sizes and sampled words, not every word."""
+    if isinstance(operator, HipCsrOp):
+        return operator
+    import scipy.sparse as sp
+    if not sp.issparse(operator) or operator.format not in ("csr", "csc"):
+        raise TypeError("operator must be a tpl_amd.HipCsrOp or a scipy CSR / CSC matrix")
+    key = operand_key(operator)
+    slot = getattr(_uploaded, "slot", None)
+    if slot is None or slot[0] != key:
+        _uploaded.slot = None  # free the previous upload before the new one
+        _uploaded.slot = (key, _upload(operator, device))
+    return _uploaded.slot[1]
+
+
+def refresh_uploaded() -> None:
+    """Forget this thread's upload of a caller's matrix: the next call uploads it again."""
+    _uploaded.slot = None

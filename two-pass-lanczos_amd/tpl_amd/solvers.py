@@ -5,7 +5,9 @@
 
 Same argument meaning and error behaviour as the reference (the ``stack``
 workspace argument has no counterpart: the device workspace belongs to the
-operator). ``f_tk_solver`` is a callable ``(alphas, betas) -> y'`` or a built-in
+operator). ``operator`` is a ``HipCsrOp`` (upload once) or the caller's own scipy CSR / CSC
+matrix (uploaded on first use and re-used while unchanged: ``operator.as_operator``).
+``f_tk_solver`` is a callable ``(alphas, betas) -> y'`` or a built-in
 from :mod:`tpl_amd.ftk` (``"inv"``, ``"exp"``, ``"sq"``). Returns x_k with the
 shape of ``b`` flattened to (n,) — numpy for host ``b``, torch CUDA for device ``b``.
 """
@@ -14,12 +16,11 @@ from __future__ import annotations
 from . import _lib, ftk
 from ._vec import Vec
 from .error import LanczosError, check
-from .operator import HipCsrOp
+from .operator import as_operator
 
 
 def _run(fn, operator, b, k, f_tk_solver):
-    if not isinstance(operator, HipCsrOp):
-        raise TypeError("operator must be a tpl_amd.HipCsrOp")
+    operator = as_operator(operator)
     bv = Vec(b)
     x = bv.empty(operator.nrows())
     fptr, keep = ftk.resolve(f_tk_solver)
