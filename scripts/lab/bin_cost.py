@@ -91,6 +91,42 @@ def features(pa, bins, cnt):
 NAMES = ["entries", "lines", "pieces", "big", "small", "single", "passes_small", "longest"]
 
 
+def layout_cost(pa, b):
+    """tpl_layout.cpp's predicted bin cost (line units): 228 per piece-sum round of the
+    wave tasks + the distinct lines."""
+    if not b:
+        return 0
+    big = sum(1 for p in b if p[2] - p[1] > BIG)
+    small = len(b) - big
+    rounds = (-(-big // 4) + -(-small // 8) + 3) // 4
+    cols = np.concatenate([pa.indices[p[1]:p[2]] for p in b])
+    return 228 * rounds + len(np.unique(cols >> 4))
+
+
+def place_light_on_crowded(pa, bins, M, S):
+    """tpl_layout.cpp bin_balance 2: the first fit's bins, the lightest of each slice on the
+    crowded CU positions (m mod 32 < M mod 32, S = 8, M > 32)."""
+    if not (S == 8 and M > 32 and M % 32):
+        return bins
+    crowded = [m % 32 < M % 32 for m in range(M)]
+    out = []
+    for bs in bins:
+        bs = bs + [[] for _ in range(M - len(bs))]
+        cost = [layout_cost(pa, b) for b in bs]
+        order = sorted(range(M), key=lambda m: cost[m])  # stable
+        nc = sum(crowded)
+        light, rest = sorted(order[:nc]), sorted(order[nc:])
+        il = ir = 0
+        nb = []
+        for m in range(M):
+            if crowded[m]:
+                nb.append(bs[light[il]]); il += 1
+            else:
+                nb.append(bs[rest[ir]]); ir += 1
+        out.append(nb)
+    return out
+
+
 def main():
     npz = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "gpurun_out/diag/pass1_stamps.npz")
     pa, sch = headline_matrix()
@@ -98,6 +134,8 @@ def main():
     per_slice, cnt = pieces(pa, sch)
     bins = [first_fit(p) for p in per_slice]
     M = max(len(b) for b in bins)
+    if os.environ.get("MODE", "2") == "2":
+        bins = place_light_on_crowded(pa, bins, M, S)
     print(f"slices {S}, bins per slice {[len(b) for b in bins]}, M = {M}")
     feat = np.zeros((S * M, len(NAMES)))
     for s in range(S):

@@ -165,7 +165,20 @@ def test_step_samples_live_pass_one(kkt50k, k):
     solvers.lanczos_two_pass(op, b, k, ftk.INV)
     with pytest.raises(tpl_amd.TplError):
         op.step_samples()
+    # a re-orthogonalised standard pass and an untimed one-graph solve clear
+    # the stamps of an earlier timed solve too
+    op.set_device_ftk(2)
+    solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    assert op.step_samples()[2] == 8
+    tpl_amd.algorithms.lanczos_standard(op, b, k, reorthogonalize=True)
+    with pytest.raises(tpl_amd.TplError):
+        op.step_samples()
+    solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    assert op.step_samples()[2] == 8
     op.enable_timing(False)
+    solvers.lanczos_two_pass(op, b, k, ftk.INV)
+    with pytest.raises(tpl_amd.TplError):
+        op.step_samples()
 
 
 def test_device_inv_zero_b_error(kkt5k):

@@ -101,6 +101,7 @@ constexpr int kBinBatch = kBinMin / kTPB;  // entries per thread per load batch
 constexpr bool kPackedEntries = TPL_PACKED_ENTRIES != 0;
 constexpr bool packed_chunk_width(int w) { return kPackedEntries && (w == 1 || w == 2 || w == 4); }
 constexpr int kLongEpiRows = kTPB;  // one replicated long row per thread (k_long_epi_*)
+constexpr int kPbRanks = 8;          // most ranks whose norm partials k_p1_spmv reduces itself
 constexpr int kWinMax = 2048;        // short-chunk column window in LDS: at most this many columns
 constexpr int kWinLoads = kWinMax / 256;  // window loads per thread
 constexpr int kBinMax = 7936;        // LDS bound: 62 KiB of staged products (+1 KiB starts)
@@ -156,6 +157,10 @@ struct CsrDev {
   int32_t NA;               // #alpha partials = n_chunks + n_long
   int32_t NA_r;             // #alpha partials the reducing kernel reads (NA, or more, see DevState)
   int32_t G2_r;             // #norm partials the reducing kernel reads (G2, or #ranks)
+  int32_t pb_ld;            // > 0 (replicated partition, round 6): Pb_r holds every rank's
+                            // G2 norm partials, pb_ld apart (zero-padded), all-gathered;
+                            // k_p1_spmv reduces each rank's to its total itself (no
+                            // rank-total launch). 0: Pb_r holds G2_r partials / totals
   int32_t n_slices;         // column slices of the long rows (1, 2, 4 or 8 <= kSlices)
   int64_t n;
   int64_t E;                // elements per workgroup of the element-wise kernels

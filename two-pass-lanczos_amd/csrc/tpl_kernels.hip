@@ -95,7 +95,8 @@ __device__ __forceinline__ void p1_spmv_body(const CsrDev& A, const DevState& S,
                                              const double* __restrict__ r_prev,
                                              double* __restrict__ W, double* __restrict__ Vcol,
                                              int j, unsigned long long* stamp, double* red,
-                                             double* redb, double* lds) {
+                                             double* redb, double* lds,
+                                             double* redr = nullptr) {
   // every kernel argument in ONE scalar round trip, the launch stamp's pointer included:
   // a branch on an argument before this point (the stamp test) split the loads into three
   // dependent round trips ahead of the first vector load (ISA, round 6)
@@ -103,8 +104,17 @@ __device__ __forceinline__ void p1_spmv_body(const CsrDev& A, const DevState& S,
   asm volatile("" ::"s"(S.Pb_r), "s"(S.flags), "s"(S.norms), "s"(S.betas), "s"(S.Pa), "s"(A.G2_r),
                "s"(xsrc), "s"(r_cur), "s"(r_prev), "s"(W), "s"(Vcol), "s"(j), "s"(stamp));
   launch_stamp(stamp);
-  PartialRegs<NBP> pr;
-  load_partials(S.Pb_r, A.G2_r, pr);
+  PartialRegs<(NBP > 0 ? NBP : -NBP)> pr;
+  if constexpr (NBP > 0) {
+    load_partials(S.Pb_r, A.G2_r, pr);
+  } else {
+    // NBP = -kPbRanks (replicated partition, round 6): every rank's norm partials,
+    // all-gathered pb_ld apart and zero-padded; lane t loads partial t of each rank
+    const int ld = A.pb_ld, R = A.G2_r;
+#pragma unroll
+    for (int r = 0; r < -NBP; ++r)
+      pr.v[r] = S.Pb_r[(size_t)clampi(r, R - 1) * ld + clampi((int)threadIdx.x, ld - 1)];
+  }
   // the stop flag and beta_{j-2} with the partials, ahead of the entries and gathers:
   // read later, their wait would drain every gather in flight before the beta chain
   int stop0 = S.flags[0];
@@ -139,8 +149,32 @@ __device__ __forceinline__ void p1_spmv_body(const CsrDev& A, const DevState& S,
       double sq = 0.0;
       if ((int)threadIdx.x < A.G2_r) sq = sq + pr.v[0];
       beta = sqrt(block_sum_tail(sq, redb));
-    } else {  // any count (more than 256 NBP in batches)
+    } else if constexpr (NBP > 1) {  // any count (more than 256 NBP in batches)
       beta = sqrt(finish_partials(S.Pb_r, A.G2_r, pr, redb));
+    } else {
+      // each rank's total by the tree the rank-total launch applied (k_reorth_reduce:
+      // s = 0; s += P[t]; wave sums; (S0 + S1) + (S2 + S3) — the zero padding adds +0.0 to
+      // +0.0), then the R totals exactly as the one-partial path above reduces the
+      // all-gathered totals: the bits of the rank-total launch + all-gather, one launch
+      // less per pass-one step. One barrier more than that path; it waits
+      // for LDS traffic only, never for the gathers in flight.
+      const int R = A.G2_r, ld = A.pb_ld;
+#pragma unroll
+      for (int r = 0; r < -NBP; ++r) {
+        if (r < R) {  // uniform
+          double sr = 0.0;
+          if ((int)threadIdx.x < ld) sr = sr + pr.v[r];
+          sr = wave_sum(sr);
+          if ((threadIdx.x & 63) == 0) redr[4 * r + (threadIdx.x >> 6)] = sr;
+        }
+      }
+      __syncthreads();
+      double sq = 0.0;
+      if ((int)threadIdx.x < R) {
+        const double* q = redr + 4 * threadIdx.x;
+        sq = sq + ((q[0] + q[1]) + (q[2] + q[3]));
+      }
+      beta = sqrt(block_sum_tail(sq, redb));
     }
     if (beta <= kBreakdownTol) {
       // j == 1: zero b -> InputError (src/algorithms/mod.rs:267-273);
@@ -181,6 +215,20 @@ __global__ __launch_bounds__(kTPB, p1_min_waves(F, 1)) void k_p1_spmv(CsrDev A, 
   __shared__ double red[4], redb[4];
   extern __shared__ double lds[];
   p1_spmv_body<F, 1>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp, red, redb, lds);
+}
+// ... every rank's norm partials, gathered (replicated partition: CsrDev::pb_ld) ...
+template <int F>
+__global__ __launch_bounds__(kTPB, p1_min_waves(F, 1)) void k_p1_spmv_gp(CsrDev A, DevState S,
+                                                  const double* __restrict__ xsrc,
+                                                  const double* __restrict__ r_cur,
+                                                  const double* __restrict__ r_prev,
+                                                  double* __restrict__ W,
+                                                  double* __restrict__ Vcol, int j,
+                                                  unsigned long long* stamp) {
+  __shared__ double red[4], redb[4], redr[4 * kPbRanks];
+  extern __shared__ double lds[];
+  p1_spmv_body<F, -kPbRanks>(A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp, red, redb, lds,
+                             redr);
 }
 // ... and more (four per thread first, the rest in batches; the 5M-arc instance's 1,024
 // row blocks)
@@ -1324,6 +1372,8 @@ hipError_t p1_spmv(const CsrDev& A, const DevState& S, const double* xsrc, const
                    const double* r_prev, double* W, double* Vcol, int j, hipStream_t s,
                    unsigned long long* stamp) {
   if (spmv_grid(A) <= 0) return hipGetLastError();
+  if (A.pb_ld > 0)
+    return TPL_LAUNCH_CW(k_p1_spmv_gp, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp);
   if (A.G2_r <= kTPB)
     return TPL_LAUNCH_CW(k_p1_spmv, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp);
   return TPL_LAUNCH_CW(k_p1_spmv_wide, A, s, A, S, xsrc, r_cur, r_prev, W, Vcol, j, stamp);

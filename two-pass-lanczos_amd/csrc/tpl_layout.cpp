@@ -447,6 +447,11 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   // pure latency, and more blocks in flight hide it (measured, configs[1] 50k arcs k =
   // 200: 512 rows 2.50 ms per solve, 1024 2.52, 2048 2.54; the headline 500k: 2048 9.93,
   // 1024 9.98, 512 10.42 — profiles/r03_small_n_lab.txt)
+  elem_geometry(n, sp, L.G2, L.E);
+  return L;
+}
+
+void elem_geometry(int64_t n, const SchedParams& sp, int32_t& G2, int64_t& E) {
   int64_t er = kElemRows;
   if (sp.elem_rows > 0) {
     er = ((sp.elem_rows + 511) / 512) * 512;
@@ -454,10 +459,9 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
     while (er > 512 && (n + er - 1) / er < kElemMinBlocks) er /= 2;
   }
   const int64_t g2 = (n + er - 1) / er;
-  L.G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
-  const int64_t per = (n + L.G2 - 1) / L.G2;
-  L.E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
-  return L;
+  G2 = (int)std::max<int64_t>(1, std::min<int64_t>(sp.max_g2, g2));
+  const int64_t per = (n + G2 - 1) / G2;
+  E = std::max<int64_t>(512, ((per + 511) / 512) * 512);
 }
 
 // The CSR rules of every entry point that takes a matrix: row_ptr (n + 1 entries) starts

@@ -28,10 +28,10 @@ struct SchedParams {
                                     // per bin (their 16-lane sums run kTPB / 16 per pass)
   int bin_small = 0;                // > 0: at most this many other pieces per bin (their
                                     // 8-lane sums run kTPB / 8 per pass)
-  int bin_balance = 1;              // bins per slice after the first fit (tpl_layout.cpp):
-                                    // 0 the first fit, 1 the cost-balanced contiguous cut,
-                                    // 2 the first fit with its lightest bins moved to the
-                                    // crowded CU positions
+  int bin_balance = 2;              // bins per slice after the first fit (tpl_layout.cpp):
+                                    // 0 the first fit, 1 the cost-balanced contiguous cut
+                                    // (lab; measured slower), 2 the first fit with its
+                                    // lightest bins on the crowded CU positions (default)
   double bin_crowd = 1.0;           // bin_balance 1: cost cap of a crowded position / of
                                     // the others
 };
@@ -171,6 +171,10 @@ void permute_csr(int64_t n, const std::vector<int32_t>& rp, const std::vector<in
 // 0 and is monotone, col_idx is non-NULL when row_ptr[n] > 0, and every row's columns lie
 // in [0, n_cols) strictly ascending.
 void check_csr(int64_t n, int64_t n_cols, const int64_t* row_ptr, const int32_t* col_idx);
+
+// Element-wise workgroups of an operator of n rows (build_layout's rule): G2 blocks of E
+// rows each. Every rank of a partition can compute every other rank's count.
+void elem_geometry(int64_t n, const SchedParams& sp, int32_t& G2, int64_t& E);
 
 // n: rows of this operator (this rank's block); n_glob: columns of A (slice bounds are
 // taken on global column indices, so a partition of one rank reproduces the single-GPU

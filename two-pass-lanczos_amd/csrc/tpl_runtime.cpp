@@ -188,6 +188,9 @@ struct tpl_op_s {
                                     // together); pass two: nranks x (n_long + 1)
   int32_t y_ld1 = 0;                // n_long + the most chunks of any rank
   std::vector<int32_t> nch;         // chunks (alpha partials) of every rank
+  std::vector<int32_t> g2s;         // norm partials (element-wise blocks) of every rank
+  int32_t pb_ld = 0;                // > 0: every rank's norm partials all-gathered (CsrDev::pb_ld)
+  double* d_pball = nullptr;        // [nranks x pb_ld] gathered norm partials (pb_ld > 0)
   int32_t* d_nch = nullptr;
   // halo-exchange row blocks (tpl_dist_op_create_halo): the gathered vector is
   // [own block (ld) | nranks x hH halo slots]; rank q's slot holds the hH_q <= hH rows of
@@ -307,6 +310,7 @@ CsrDev csr_dev(const tpl_op_s* op, bool pass1 = false) {
   A.NA = A.n_chunks + A.n_long;
   A.NA_r = op->dist ? op->dist->nranks + (op->hybrid ? long_epi_blocks(op) : 0) : A.NA;
   A.G2_r = op->dist ? op->dist->nranks : A.G2;
+  A.pb_ld = op->pb_ld;
   A.long_defer = op->hybrid ? 1 : 0;
   A.y_ld = pass1 && op->hybrid ? op->y_ld1 : (int32_t)L.lrows.size() + 1;
   A.ypart = op->hybrid ? op->d_yall + (size_t)op->dist->rank * A.y_ld : nullptr;
@@ -391,6 +395,11 @@ void rebuild_schedule(tpl_op_s* op) {
   // rank's local columns (its CSR is stored in local indices)
   op->lay = build_layout(op->n, op->hybrid ? op->n : op->n_glob, p ? prp : op->h_rowptr,
                          p ? pcol : op->h_col, p ? pval : op->h_val, sp, cmap);
+  // the replicated partition's ranks agree on every rank's element-wise block count (the
+  // gathered norm partials, the alpha partial counts): a layout that changed it is refused
+  if (op->hybrid && !op->g2s.empty() && op->lay.G2 != op->g2s[op->dist->rank])
+    fail(TPL_ERR_UNSUPPORTED, "replicated partition: the element-wise blocks must stay those "
+                              "every rank computed from the split");
   if (op->plan_only) return;  // tpl_plan_create: the layout is all a plan holds
   const Layout& L = op->lay;
   upload(op, &op->d_perm, op->perm);
@@ -426,8 +435,8 @@ void rebuild_schedule(tpl_op_s* op) {
     upload(op, reinterpret_cast<double**>(&op->d_bval), to_device_order(L.b_val, bidx));
   upload(op, &op->d_bseg, L.b_seg);
   upload(op, &op->d_bhdr, L.b_hdr);
-  // piece slots, and the arrival counters of the sliced long rows (zero; they run on
-  // modulo the slice count across launches)
+  // piece slots, and the arrival counters of the sliced long rows (zero; each wraps at
+  // its row's packed-piece count, BinSeg::pad + 1, so it runs on across launches)
   upload(op, &op->d_P, std::vector<double>(std::max<size_t>(L.lrows.size() * kSlotStride, 1), 0.0));
   upload(op, &op->d_Pcnt,
          std::vector<unsigned int>(std::max<size_t>(L.lrows.size() * kCntStride, 1), 0u));
@@ -476,6 +485,10 @@ void ensure_state(tpl_op_s* op, size_t k, bool reorth = false) {
       op->S.Pa = op->d_yall + (size_t)op->dist->rank * op->y_ld1 + op->lay.lrows.size();
     op->S.Pa_r = op->dist ? op->d_rsum : op->S.Pa;
     op->S.Pb_r = op->dist ? op->d_rsum + A.NA_r : op->S.Pb;
+    if (op->pb_ld > 0) {  // the norm partials go straight into this rank's gathered segment
+      op->S.Pb = op->d_pball + (size_t)op->dist->rank * op->pb_ld;
+      op->S.Pb_r = op->d_pball;
+    }
     op->kcap = kc;
   }
   if (reorth && !op->d_Pr) {
@@ -648,9 +661,13 @@ void enqueue_reorth(tpl_op_s* op, int j, int mode) {
 void enqueue_p1_prologue(tpl_op_s* op) {
   const CsrDev A = csr_dev(op);
   HIPCHK(launch::p1_init(A, op->S, op->b, op->stream));
-  if (op->hybrid) {  // every column this rank gathers is local: only the norm totals move
-    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
-    dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+  if (op->hybrid) {  // every column this rank gathers is local: only the norm partials move
+    if (op->pb_ld > 0) {
+      dist_allgather(op, op->d_pball, (size_t)op->pb_ld);
+    } else {
+      dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+      dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+    }
   } else if (op->dist) {
     const int R = op->dist->nranks;
     dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
@@ -680,10 +697,17 @@ void enqueue_p1_exchange_a(tpl_op_s* op, const CsrDev& A) {
 }
 void enqueue_p1_exchange_b(tpl_op_s* op, const CsrDev& A, int j) {
   if (op->hybrid) {
-    // the rank's beta total: its own one-workgroup launch (folding it into k_p1_axpy's
-    // last arriver measured slower, round 5: DESIGN.md §6.3)
-    dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
-    dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+    if (op->pb_ld > 0) {
+      // round 6: every rank's norm partials travel (pb_ld doubles per rank) and the next
+      // k_p1_spmv reduces each rank's itself — no rank-total launch between k_p1_axpy and
+      // the collective
+      dist_allgather(op, op->d_pball, (size_t)op->pb_ld);
+    } else {
+      // the rank's beta total: its own one-workgroup launch (folding it into k_p1_axpy's
+      // last arriver measured slower, round 5: DESIGN.md §6.3)
+      dist_total(op, op->S.Pb, A.G2, const_cast<double*>(op->S.Pb_r) + op->dist->rank);
+      dist_allgather(op, const_cast<double*>(op->S.Pb_r), 1);
+    }
   } else {
     const int R = op->dist->nranks;
     dist_total(op, op->S.Pb, A.G2, op->d_rsum + R + op->dist->rank);
@@ -889,6 +913,7 @@ void run_two_pass_dev(tpl_op_s* op, size_t k, int f) {
   const size_t key = 2 * k + (size_t)f;  // one graph per (k, f)
   const bool elim = f == kDevInv;  // T_k's LU eliminated during pass one
   if (!op->timing) {
+    op->p1_samples = 0;  // the untimed graph records no launch stamps
     run_graph(op, kGTwoPassDev, key, [&] {
       enqueue_pass1(op, k, false, false, elim);
       enqueue_ftk_dev(op, k, f);
@@ -921,10 +946,10 @@ void run_pass_one(tpl_op_s* op, const double* b, size_t k, int mem, bool storeV,
   ensure_state(op, k, reorth);
   if (storeV) ensure_basis(op, k);
   upload_vec(op, op->b, b, mem);
+  op->p1_samples = 0;  // no pass run here records launch stamps (tpl_op_step_samples)
   if (reorth) {
     enqueue_pass1(op, k, true, reorth); // eager: reorth launch counts vary with j
   } else {
-    op->p1_samples = 0;  // this pass records no launch stamps (tpl_op_step_samples)
     if (op->timing) HIPCHK(hipEventRecord(op->tev[0], op->stream));
     const int kind = storeV ? (elim ? kGStandardElim : kGStandard) : (elim ? kGPass1Elim : kGPass1);
     run_graph(op, kind, k, [&] { enqueue_pass1(op, k, storeV, false, elim); });
@@ -1025,6 +1050,19 @@ void init_op(tpl_op_s* op) {
       const size_t ya = nr * (size_t)std::max<int64_t>(op->y_ld1, (int64_t)op->lay.lrows.size() + 1);
       dev_alloc(op, &op->d_yall, ya * sizeof(double));
       HIPCHK(hipMemset(op->d_yall, 0, ya * sizeof(double)));
+      // the β stage all-gathers every rank's norm partials (each rank computes all ranks'
+      // counts from the global split) and k_p1_spmv reduces each rank's with the tree the
+      // rank-total launch applied — one launch less per pass-one step, the same bits —
+      // while they fit one load per lane and rank (≤ kPbRanks ranks, ≤ kTPB partials)
+      if ((int)op->g2s.size() != op->dist->nranks ||
+          op->g2s[op->dist->rank] != op->lay.G2)
+        fail(TPL_ERR_UNSUPPORTED, "replicated partition: block counts disagree with the layout");
+      const int32_t g2max = *std::max_element(op->g2s.begin(), op->g2s.end());
+      if (op->dist->nranks <= kPbRanks && g2max <= kTPB) {
+        op->pb_ld = g2max;
+        dev_alloc(op, &op->d_pball, nr * (size_t)g2max * sizeof(double));
+        HIPCHK(hipMemset(op->d_pball, 0, nr * (size_t)g2max * sizeof(double)));
+      }
     }
   }
   HIPCHK(hipEventCreate(&op->ev0));
@@ -1148,8 +1186,12 @@ void fill_replicated(tpl_op_s* op, int R, int me, int64_t n, const int64_t* row_
   op->nnz = (int64_t)op->h_col.size();
   op->sp.long_from = ns;
   op->nch.resize(R);
-  for (int r = 0; r < R; ++r)
+  op->g2s.resize(R);
+  for (int r = 0; r < R; ++r) {
     op->nch[r] = (int32_t)((cut[r + 1] - cut[r] + kChunkRows - 1) / kChunkRows);
+    int64_t E = 0;
+    elem_geometry(cut[r + 1] - cut[r] + nl, op->sp, op->g2s[r], E);
+  }
 }
 
 // Host half of a row-block rank from the WHOLE matrix (TPL_PLAN_ROWS, TPL_PLAN_HALO,
