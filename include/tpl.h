@@ -109,7 +109,9 @@ int64_t tpl_op_nnz(tpl_op_t op);
  * evaluated f(T_k) on the device (one graph, no host round trip), bit 6: rows held in the locality order
  * (tpl_op_set_reorder, tpl_op_permutation; on a replicated-long-row partition the
  * rank's own short rows are in that order and tpl_op_local_rows, not
- * tpl_op_permutation, reports it). -1 if op is NULL.                               */
+ * tpl_op_permutation, reports it), bit 7: a replicated-long-row partition whose ranks
+ * all-gather their norm partials and reduce them inside pass one's SpMV (no rank-total
+ * launch). -1 if op is NULL.                                         */
 int tpl_op_flags(tpl_op_t op);
 /* Locality order (single-GPU operators; rebuilds the layout). mode 1: the device
  * holds P A P^T, the short rows sorted by the long rows (hub columns) they reference

@@ -88,6 +88,9 @@ def _check_exchange_profile(rs):
             nl = len(r["s_long"])
             nch = max(-(-(len(q["rows"]) - nl) // 512) for q in rs)
             assert b2 == 8 * R * (nl + 1) and b1 == 8 * R * (nl + nch + 1)
+            # tpl_op_flags bit 7: the norm partials travel gathered and pass one's SpMV
+            # reduces them (R <= kPbRanks, the 5k KKT's long-row partials fit one block)
+            assert int(r["flags"]) & 128
         elif str(r["mode"]) == "halo":  # the halo slots (none with one rank)
             assert b1 - b2 == 16 * R and b2 % (8 * R) == 0 and (b2 > 0) == (R > 1)
         else:

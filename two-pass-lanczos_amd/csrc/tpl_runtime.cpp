@@ -1392,7 +1392,7 @@ int tpl_op_flags(tpl_op_t op) {
   if (!op) return -1;
   return (op->dist ? 1 : 0) | (op->eager ? 2 : 0) | (op->lay.val_i8 ? 4 : 0) |
          (op->lay.s_col16 ? 8 : 0) | (op->lay.b_col16 ? 16 : 0) | (op->last_one_graph ? 32 : 0) |
-         (!op->perm.empty() || op->local_order ? 64 : 0);
+         (!op->perm.empty() || op->local_order ? 64 : 0) | (op->pb_ld > 0 ? 128 : 0);
 }
 
 tpl_status tpl_op_set_reorder(tpl_op_t op, int mode) {
