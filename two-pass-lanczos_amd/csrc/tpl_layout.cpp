@@ -212,10 +212,13 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
   // 0-3 hold three bins and three chunks, the rest two bins and four chunks). Those
   // positions m (m mod 32 < M mod 32) are "crowded"; the cut gives them a smaller cost cap
   // (crowd x the others').
+  // With S = 8 TX > 8 slices an XCD runs TX slices, bin m of slice s as its workgroup
+  // TX m + s mod TX (tpl_kcommon.h spmv_block_impl), TX M bins per XCD.
   constexpr int kCuClasses = 32;  // CUs per XCD (MI355X: 256 CUs / 8 XCDs)
-  auto crowded = [&](int32_t m) {
-    return S == kSlices && L.M > kCuClasses && L.M % kCuClasses != 0 &&
-           m % kCuClasses < L.M % kCuClasses;
+  const int TX = S >= 8 ? S / 8 : 0;  // slices per XCD (0: S < 8, no crowding rule)
+  auto crowded = [&](int32_t m, int s) {
+    const int32_t Q = TX * L.M, q = TX * m + (TX > 0 ? s % TX : 0);
+    return TX > 0 && Q > kCuClasses && Q % kCuClasses != 0 && q % kCuClasses < Q % kCuClasses;
   };
   auto pack = [&](int s, int64_t cost_cap, double crowd,
                   std::vector<std::vector<std::pair<int32_t, int32_t>>>& out,
@@ -252,7 +255,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
                 (!big && sp.bin_small > 0 && nsmall == sp.bin_small) ||
                 (cost_cap >= 0 &&
                  rounds(nb, ns) * kRoundCost + nlines + fresh >
-                     (crowded((int32_t)out.size() - 1) ? (int64_t)(crowd * (double)cost_cap)
+                     (crowded((int32_t)out.size() - 1, s) ? (int64_t)(crowd * (double)cost_cap)
                                                        : cost_cap));
         if (close) fresh = fresh_lines(q0, q1, false);  // the piece against an empty bin
       }
@@ -305,7 +308,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
     int64_t lo = 0, hi = 0;  // hi: a cap the first fit's cut meets on every position
     for (size_t m = 0; m < bins[s].size(); ++m) {
       const int64_t c = bin_cost(s, bins[s][m]);
-      hi = std::max(hi, crowded((int32_t)m) ? (int64_t)std::ceil((double)c / sp.bin_crowd) + 1 : c);
+      hi = std::max(hi, crowded((int32_t)m, s) ? (int64_t)std::ceil((double)c / sp.bin_crowd) + 1 : c);
     }
     while (lo < hi) {
       const int64_t mid = lo + (hi - lo) / 2;
@@ -315,7 +318,8 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
     }
     pack(s, hi, sp.bin_crowd, bins[s], fill[s]);
   }
-  if (sp.bin_balance == 2 && nlb > 0 && L.M > kCuClasses && L.M % kCuClasses != 0 && S == kSlices) {
+  if (sp.bin_balance == 2 && nlb > 0 && TX > 0 && TX * L.M > kCuClasses &&
+      (TX * L.M) % kCuClasses != 0) {
     for (int s = 0; s < S; ++s) {
       bins[s].resize(L.M);
       fill[s].resize(L.M, 0);
@@ -327,7 +331,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
       }
       std::stable_sort(ord.begin(), ord.end(), [&](int32_t a, int32_t b) { return cost[a] < cost[b]; });
       int32_t ncrowd = 0;
-      for (int32_t m = 0; m < L.M; ++m) ncrowd += crowded(m);
+      for (int32_t m = 0; m < L.M; ++m) ncrowd += crowded(m, s);
       std::vector<int32_t> light(ord.begin(), ord.begin() + ncrowd), rest(ord.begin() + ncrowd, ord.end());
       std::sort(light.begin(), light.end());
       std::sort(rest.begin(), rest.end());
@@ -335,7 +339,7 @@ Layout build_layout(int64_t n, int64_t n_glob, const std::vector<int32_t>& rp,
       std::vector<int32_t> nf(L.M);
       size_t il = 0, ir = 0;
       for (int32_t m = 0; m < L.M; ++m) {
-        const int32_t from = crowded(m) ? light[il++] : rest[ir++];
+        const int32_t from = crowded(m, s) ? light[il++] : rest[ir++];
         nb[m] = std::move(bins[s][from]);
         nf[m] = fill[s][from];
       }
