@@ -64,6 +64,8 @@ WORKLOADS = {
                                    mode="replicated", nranks=8),
     # the headline partitioned (bench.py --gpus N, N > 1: the line's `value`, strong
     # scaling of configs[2]; --dist-mode auto takes the replicated long rows for the KKT)
+    "configs2_replicated_N1": dict(arcs=500000, k=500, f="inv", solver="partition",
+                                   mode="replicated", nranks=1),
     "configs2_replicated_N2": dict(arcs=500000, k=500, f="inv", solver="partition",
                                    mode="replicated", nranks=2),
     "configs2_replicated_N4": dict(arcs=500000, k=500, f="inv", solver="partition",
