@@ -266,3 +266,32 @@ def test_config4_5m_partitions_two_ranks(tmp_path, mode, op5m, kkt5m):
     assert np.array_equal(xd, xo)
     assert np.array_equal(xd, _assemble(rs, "x2", a.shape[0]))
     np.testing.assert_allclose(rs[0]["be"][:12], dec.betas[:12], rtol=1e-10)
+
+
+@pytest.mark.timeout(600)
+def test_replicated_wide_blocks_two_ranks(tmp_path):
+    """The replicated partition's widened element-wise blocks (tpl_runtime.cpp
+    fill_replicated: at most 256 norm partials per rank when that needs <= 4,096 rows per
+    block — configs[4] at N = 8): a 1.5M-arc synthetic instance over two ranks holds
+    ~750k rows per rank, 367 partials at the default 2,048 rows, so the rule widens the
+    blocks to 3,072 rows (245 partials) and pass one's SpMV reduces the gathered partials
+    itself (tpl_op_flags bit 7). k = 30: alphas, betas and x BIT FOR BIT against the
+    partitioned order restated on the CPU, identical on both ranks."""
+    from partition_oracle import PartitionOracle
+    from test_gpu_dist import _assemble, _run_ranks
+    arcs = 1500000
+    a = load_kkt(arcs, str(tmp_path)).a
+    b = harness_b(a)
+    k = 30
+    rs = _run_ranks(str(tmp_path), 2, "host", mode="replicated", arcs=arcs, k=k)
+    for r in rs:
+        assert int(r["flags"]) & 128, "gathered norm partials not used"
+        assert int(r["s_E"]) == 3072 and int(r["s_G2"]) <= 256, (int(r["s_E"]), int(r["s_G2"]))
+    assert np.array_equal(rs[0]["al"], rs[1]["al"]) and np.array_equal(rs[0]["be"], rs[1]["be"])
+    po = PartitionOracle(a, rs, "replicated")
+    al, be, s, bn = po.pass_one(b, k)
+    assert int(rs[0]["steps"]) == s
+    assert np.array_equal(rs[0]["al"], al) and np.array_equal(rs[0]["be"], be)
+    xo = po.pass_two(b, al, be, s, bn, ftk.INV(al, be) * bn)
+    xd = _assemble(rs, "x1", a.shape[0])
+    assert np.array_equal(xd, xo)

@@ -1192,6 +1192,26 @@ void fill_replicated(tpl_op_s* op, int R, int me, int64_t n, const int64_t* row_
     int64_t E = 0;
     elem_geometry(cut[r + 1] - cut[r] + nl, op->sp, op->g2s[r], E);
   }
+  // Up to kPbRanks ranks: element-wise blocks wide enough that no rank holds more than kTPB
+  // norm partials, so pass one's SpMV reduces every rank's gathered partials itself (one
+  // load per lane and rank) and no rank-total launch remains — when that needs at most
+  // 2 kElemRows rows per block. Measured on the 5M-arc instance (round 6, rank shares
+  // through one RCCL rank, profiles/r06_rank_share_5m_wide.txt): N = 8, 306 -> 246
+  // partials at 2,560 rows per block, slowest share 14.35 -> 13.78 ms; N = 4, 5,120 rows
+  // per block, 20.69 -> 21.29 ms (k_p1_axpy's wider blocks cost more than the launch), so
+  // not applied there. Every rank applies the same rule to the same split, so all agree
+  // on every rank's count.
+  int64_t rows_max = 0;
+  for (int r = 0; r < R; ++r) rows_max = std::max<int64_t>(rows_max, cut[r + 1] - cut[r] + nl);
+  const int64_t er_gp = (((rows_max + kTPB - 1) / kTPB) + 511) / 512 * 512;
+  if (R <= kPbRanks && op->sp.elem_rows <= 0 && er_gp <= 2 * kElemRows &&
+      *std::max_element(op->g2s.begin(), op->g2s.end()) > kTPB) {
+    op->sp.elem_rows = (int)er_gp;
+    for (int r = 0; r < R; ++r) {
+      int64_t E = 0;
+      elem_geometry(cut[r + 1] - cut[r] + nl, op->sp, op->g2s[r], E);
+    }
+  }
 }
 
 // Host half of a row-block rank from the WHOLE matrix (TPL_PLAN_ROWS, TPL_PLAN_HALO,
